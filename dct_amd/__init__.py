@@ -1,0 +1,169 @@
+"""dct_amd -- MI355X-native 8x8 DCT + quantization hot path of erkinov-wtf/dct.
+
+Python host over the C-ABI of ``libdct_amd.so`` (include/dct_amd.h, and the
+reference's per-block API include/dct.h / include/quantization.h).  PyTorch is
+used only as the owner of device memory and streams: tensors are handed to the
+library as raw pointers on torch's current HIP stream, so torch.cuda.Event
+timing sees the kernels.
+
+The library is REQUIRED: importing a compute entry point without a built
+``libdct_amd.so`` raises -- there is no CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdct_amd.so")
+
+# synthetic frame kinds (include/dct_amd.h, dctq_synth)
+KINDS = {"uniform": 0, "smooth": 1, "const": 2, "extreme": 3}
+
+
+class DctqError(RuntimeError):
+    pass
+
+
+class _Plane(C.Structure):
+    _fields_ = [("pixels", C.c_void_p), ("stride", C.c_longlong), ("frame_stride", C.c_longlong),
+                ("width", C.c_int), ("height", C.c_int), ("nframes", C.c_int)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libdct_amd.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DctqError(f"{LIB_PATH} is missing: run `python -m dct_amd.build` (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        vp, i, ll = C.c_void_p, C.c_int, C.c_longlong
+        sig = {
+            "dctq_plan_create": ([i, i, C.POINTER(vp)], i),
+            "dctq_plan_destroy": ([vp], None),
+            "dctq_plan_set_fallback_counter": ([vp, vp], i),
+            "dctq_forward_quant": ([vp, C.POINTER(_Plane), vp, vp, vp], i),
+            "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
+            "dctq_inverse": ([vp, vp, vp, ll, vp, vp], i),
+            "dctq_synth": ([C.c_uint64, i, C.POINTER(_Plane), vp], i),
+            "dctq_error_string": ([i], C.c_char_p),
+            "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
+            "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
+            "dctq_synchronize": ([vp], i),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise DctqError(f"dctq error {rc}: {lib().dctq_error_string(rc).decode()}")
+
+
+def _stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def plane_desc(px, width: int = None, height: int = None):
+    """Describe a uint8 CUDA tensor [H, W] or [F, H, W] (rows may be padded: stride = px.stride(-2))."""
+    import torch
+    if px.dtype != torch.uint8 or not px.is_cuda:
+        raise DctqError("pixels must be a uint8 tensor on a HIP device")
+    if px.dim() == 2:
+        px = px.unsqueeze(0)
+    if px.dim() != 3 or px.stride(-1) != 1:
+        raise DctqError("pixels must be [H, W] or [F, H, W] with unit column stride")
+    f, h, w = px.shape
+    return _Plane(px.data_ptr(), px.stride(1), px.stride(0) if f > 1 else px.stride(1) * h,
+                  width if width is not None else w, height if height is not None else h, f)
+
+
+class Plan:
+    """Tables for one (quality, adaptive) configuration on the current device
+    (quant_init(8, quality, adaptive) semantics, src/quantization.c:19-41)."""
+
+    def __init__(self, quality: int = 50, adaptive: bool = False):
+        self.quality, self.adaptive = quality, bool(adaptive)
+        h = C.c_void_p()
+        _check(lib().dctq_plan_create(int(quality), int(bool(adaptive)), C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().dctq_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_fallback_counter(self, counter):
+        """counter: int64 CUDA tensor of one element (or None)."""
+        _check(lib().dctq_plan_set_fallback_counter(self._h, C.c_void_p(counter.data_ptr()) if counter is not None else None))
+
+    # --- hot path -------------------------------------------------------
+    def forward_quant(self, px, out=None, var_num=None, stream=None):
+        """u8 [H,W] / [F,H,W] -> int16 [F*H/8*W/8, 64] quantized coefficients (bit-exact)."""
+        import torch
+        d = plane_desc(px)
+        nblk = d.nframes * (d.width // 8) * (d.height // 8)
+        if out is None:
+            out = torch.empty((nblk, 64), dtype=torch.int16, device=px.device)
+        _check(lib().dctq_forward_quant(self._h, C.byref(d), C.c_void_p(out.data_ptr()),
+                                        C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
+                                        _stream_ptr(stream)))
+        return out
+
+    def forward_float(self, px, out=None, stream=None):
+        import torch
+        d = plane_desc(px)
+        nblk = d.nframes * (d.width // 8) * (d.height // 8)
+        if out is None:
+            out = torch.empty((nblk, 64), dtype=torch.float32, device=px.device)
+        _check(lib().dctq_forward_float(self._h, C.byref(d), C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+        return out
+
+    def inverse(self, coef, var_num=None, out=None, stream=None):
+        """int16 [N, 64] -> float32 [N, 64] = dct_inverse(dequantize(coef)) + 128."""
+        import torch
+        n = coef.numel() // 64
+        if out is None:
+            out = torch.empty((n, 64), dtype=torch.float32, device=coef.device)
+        _check(lib().dctq_inverse(self._h, C.c_void_p(coef.data_ptr()),
+                                  C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
+                                  n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+        return out
+
+
+def synth(seed: int, kind, width: int, height: int, nframes: int = 1, device="cuda", stream=None, out=None):
+    """Synthetic u8 frames [F, H, W] generated on the device (oracle-identical)."""
+    import torch
+    k = KINDS[kind] if isinstance(kind, str) else int(kind)
+    if out is None:
+        out = torch.empty((nframes, height, width), dtype=torch.uint8, device=device)
+    d = plane_desc(out)
+    _check(lib().dctq_synth(C.c_uint64(seed), k, C.byref(d), _stream_ptr(stream)))
+    return out
+
+
+def debug_tables(quality: int, adaptive: bool = False):
+    """Host-only: the (w, thr, D, Q) tables a plan would upload (no GPU needed)."""
+    import numpy as np
+    w = np.zeros(64, np.float32)
+    thr = np.zeros(64, np.float32)
+    d = np.zeros(64, np.float64)
+    q = np.zeros(64, np.float64)
+    _check(lib().dctq_debug_tables(quality, int(adaptive), w.ctypes.data, thr.ctypes.data, d.ctypes.data,
+                                   q.ctypes.data))
+    return w, thr, d, q

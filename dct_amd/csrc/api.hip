@@ -1,0 +1,276 @@
+// dct_amd/csrc/api.hip -- the batched C-ABI of include/dct_amd.h.
+//
+// Host side of the hot path: builds the per-plan tables (D of src/dct.c:17-30 and
+// Q of src/quantization.c:51-99 with the reference's own expressions, so the
+// exact tie path sees bit-identical constants; the fast path's scale and guard
+// tables from the proven bound in fdct8_bound.h), validates arguments, and
+// launches the kernels of fdct8.hip / fdct8_aux.hip on the caller's stream.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "dct_amd.h"
+#include "dctq_internal.h"
+#include "fdct8_bound.h"
+#include "host_tables.h"
+
+struct dctq_plan {
+    int quality, adaptive, device;
+    dctq::FastTables fast;       // thresholds for the mode in `adaptive`
+    dctq::DevTables host;        // host copy of the device tables
+    dctq::DevTables *dev;        // device copy
+    unsigned long long *fallbacks;
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char *what, hipError_t e = hipSuccess) {
+    g_err = what;
+    if (e != hipSuccess) {
+        g_err += ": ";
+        g_err += hipGetErrorString(e);
+    }
+    return code;
+}
+#define HIPCHK(call, what)                                  \
+    do {                                                    \
+        hipError_t e_ = (call);                             \
+        if (e_ != hipSuccess) return fail(DCTQ_EHIP, what, e_); \
+    } while (0)
+}  // namespace
+
+namespace dctq {
+FastDiv make_fastdiv(uint32_t d) {
+    uint32_t s = 0;
+    while ((1ull << s) < d) ++s;
+    const uint64_t m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
+    return FastDiv{d, (uint32_t)m, s};
+}
+
+// Guard band of the fast path (DESIGN.md "Exactness").  With Y~ the fp32
+// butterfly output (|Y~ - Y| <= kErrY), w~ = fl32(S_i S_j / Q) and
+// f~ = fl(Y~ w~ - r) for r = rint(Y~ w~), the reference's quotient V = fl(ref / M)
+// satisfies |V - (r + f~)| <= B below; hence |f~| <= 0.5 - B  =>  round(V) == r.
+void fill_fast_tables(const double *q, int adaptive, FastTables *t) {
+    const double u = 0x1p-24;
+    const double rel = adaptive ? 3.0 * u + 0x1p-48 : u + 0x1p-48;
+    for (int c = 0; c < 64; ++c) {
+        const int i = c >> 3, j = c & 7;
+        const double w = kAanScale[i] * kAanScale[j] / q[c];
+        const float wf = (float)w;
+        const double wt = (double)wf;
+        const double B = 0x1p-25                        /* rounding of f~ */
+                         + kErrY[c] * wt * (1.0 + 4.0 * u) /* butterfly error, scaled */
+                         + kMaxY[c] * w * rel           /* scale-factor representation */
+                         + 1e-9 / q[c]                  /* reference's own fp64 error (< 1e-11) */
+                         + (kMaxY[c] * w + 1.0) * 0x1p-52; /* reference's division rounding */
+        double thr = (0.5 - B) * (1.0 - 0x1p-20);
+        float tf = (float)thr;
+        if ((double)tf > thr) tf = nextafterf(tf, 0.0f);
+        t->w[c] = wf;
+        t->thr[c] = tf;
+    }
+}
+}  // namespace dctq
+
+static int build_plan(const double *q, int quality, int adaptive, dctq_plan **out) {
+    if (!out) return fail(DCTQ_EINVAL, "plan pointer is NULL");
+    for (int c = 0; c < 64; ++c)
+        if (!(q[c] >= 1.0 && q[c] <= 65535.0)) return fail(DCTQ_EINVAL, "quant_matrix entries must lie in [1, 65535]");
+    int dev = 0, arch_ok = 0;
+    HIPCHK(hipGetDevice(&dev), "hipGetDevice");
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
+    arch_ok = strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    if (!arch_ok) return fail(DCTQ_ENODEV, "libdct_amd is built for gfx950 (MI355X) only");
+    dctq_plan *p = new dctq_plan();
+    p->quality = quality;
+    p->adaptive = adaptive ? 1 : 0;
+    p->device = dev;
+    p->fallbacks = nullptr;
+    dctq_host::dct_matrix(8, p->host.dct);
+    for (int c = 0; c < 64; ++c) {
+        const double s2 = kAanScale[c >> 3] * kAanScale[c & 7];
+        p->host.quant[c] = q[c];
+        p->host.dequant[c] = 1.0 / q[c];
+        p->host.s2[c] = s2;
+        p->host.iscale[c] = p->host.dequant[c] * s2;
+        p->host.qscale[c] = q[c] * s2;
+    }
+    dctq::fill_fast_tables(q, p->adaptive, &p->fast);
+    hipError_t e = hipMalloc(&p->dev, sizeof(dctq::DevTables));
+    if (e != hipSuccess) {
+        delete p;
+        return fail(DCTQ_ENOMEM, "hipMalloc(plan tables)", e);
+    }
+    e = hipMemcpy(p->dev, &p->host, sizeof(dctq::DevTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(p->dev);
+        delete p;
+        return fail(DCTQ_EHIP, "hipMemcpy(plan tables)", e);
+    }
+    *out = p;
+    return DCTQ_OK;
+}
+
+static int plane_args(const dctq_plane *s, dctq::PlaneArgs *a) {
+    if (!s || !s->pixels) return fail(DCTQ_EINVAL, "plane/pixels is NULL");
+    if (s->width <= 0 || s->height <= 0 || s->width % 8 || s->height % 8)
+        return fail(DCTQ_EINVAL, "width and height must be positive multiples of 8");
+    if (s->stride < s->width || s->stride % 8) return fail(DCTQ_EINVAL, "stride must be >= width and a multiple of 8");
+    if (((uintptr_t)s->pixels) % 8 || s->frame_stride % 8) return fail(DCTQ_EINVAL, "pixels/frame_stride must be 8-byte aligned");
+    if (s->nframes < 1) return fail(DCTQ_EINVAL, "nframes must be >= 1");
+    if (s->nframes > 1 && s->frame_stride < s->stride * (long long)s->height)
+        return fail(DCTQ_EINVAL, "frame_stride smaller than one frame");
+    const long long bw = s->width / 8, bh = s->height / 8, per = bw * bh, tot = per * s->nframes;
+    if (tot >= (1ll << 31) - 256) return fail(DCTQ_EINVAL, "more than 2^31 blocks in one call");
+    a->src = s->pixels;
+    a->stride = s->stride;
+    a->frame_stride = s->frame_stride;
+    a->bw = (int)bw;
+    a->nblk_frame = (int)per;
+    a->nblk = (int)tot;
+    a->div_bw = dctq::make_fastdiv((uint32_t)bw);
+    a->div_frame = dctq::make_fastdiv((uint32_t)per);
+    return DCTQ_OK;
+}
+
+extern "C" {
+
+int dctq_plan_create(int quality, int adaptive, dctq_plan **plan) {
+    double q[64];
+    quality = dctq_host::clamp_quality(quality);
+    dctq_host::quant_matrix(8, quality, q);
+    return build_plan(q, quality, adaptive, plan);
+}
+
+int dctq_plan_from_context(const QuantContext *qctx, dctq_plan **plan) {
+    if (!qctx || qctx->block_size != 8 || !qctx->quant_matrix) return fail(DCTQ_EINVAL, "QuantContext must be 8x8");
+    double q[64];
+    for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) q[i * 8 + j] = qctx->quant_matrix[i][j];
+    return build_plan(q, qctx->quality, qctx->adaptive, plan);
+}
+
+void dctq_plan_destroy(dctq_plan *plan) {
+    if (!plan) return;
+    (void)hipFree(plan->dev);
+    delete plan;
+}
+
+int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter) {
+    if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
+    plan->fallbacks = counter;
+    return DCTQ_OK;
+}
+
+int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num, void *stream) {
+    if (!plan || !coef) return fail(DCTQ_EINVAL, "plan/coef is NULL");
+    if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
+    dctq::PlaneArgs a;
+    int rc = plane_args(src, &a);
+    if (rc) return rc;
+    HIPCHK(dctq::launch_fdct8_quant(a, plan->fast, plan->dev, plan->adaptive, coef, var_num, plan->fallbacks,
+                                    (hipStream_t)stream),
+           "fdct8_quant launch");
+    return DCTQ_OK;
+}
+
+int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream) {
+    if (!plan || !coef) return fail(DCTQ_EINVAL, "plan/coef is NULL");
+    if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
+    dctq::PlaneArgs a;
+    int rc = plane_args(src, &a);
+    if (rc) return rc;
+    HIPCHK(dctq::launch_fdct8_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
+    return DCTQ_OK;
+}
+
+int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks, float *recon,
+                 void *stream) {
+    if (!plan || !coef || !recon) return fail(DCTQ_EINVAL, "plan/coef/recon is NULL");
+    if (plan->adaptive && !var_num) return fail(DCTQ_EINVAL, "adaptive inverse needs var_num");
+    if (nblocks < 0 || nblocks >= (1ll << 40)) return fail(DCTQ_EINVAL, "bad nblocks");
+    if (((uintptr_t)coef) % 16 || ((uintptr_t)recon) % 16) return fail(DCTQ_EINVAL, "coef/recon must be 16-byte aligned");
+    if (nblocks == 0) return DCTQ_OK;
+    HIPCHK(dctq::launch_idct8(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream),
+           "idct8 launch");
+    return DCTQ_OK;
+}
+
+int dctq_synth(uint64_t seed, int kind, const dctq_plane *dst, void *stream) {
+    if (!dst || !dst->pixels) return fail(DCTQ_EINVAL, "dst is NULL");
+    if (dst->width <= 0 || dst->height <= 0 || dst->width % 4 || dst->stride < dst->width || dst->stride % 4 ||
+        dst->nframes < 1 || ((uintptr_t)dst->pixels) % 4)
+        return fail(DCTQ_EINVAL, "bad synth plane geometry");
+    HIPCHK(dctq::launch_synth(seed, kind, (uint8_t *)dst->pixels, dst->stride, dst->frame_stride, dst->width,
+                              dst->height, dst->nframes, (hipStream_t)stream),
+           "synth launch");
+    return DCTQ_OK;
+}
+
+int dctq_device_count(int *count) {
+    HIPCHK(hipGetDeviceCount(count), "hipGetDeviceCount");
+    return DCTQ_OK;
+}
+int dctq_set_device(int device) {
+    HIPCHK(hipSetDevice(device), "hipSetDevice");
+    return DCTQ_OK;
+}
+int dctq_malloc(void **ptr, size_t bytes) {
+    HIPCHK(hipMalloc(ptr, bytes), "hipMalloc");
+    return DCTQ_OK;
+}
+int dctq_free(void *ptr) {
+    HIPCHK(hipFree(ptr), "hipFree");
+    return DCTQ_OK;
+}
+int dctq_memcpy_htod(void *dst, const void *src, size_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+    return DCTQ_OK;
+}
+int dctq_memcpy_dtoh(void *dst, const void *src, size_t bytes) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+    return DCTQ_OK;
+}
+int dctq_synchronize(void *stream) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+    return DCTQ_OK;
+}
+
+const char *dctq_error_string(int code) {
+    if (code == DCTQ_OK) return "ok";
+    if (!g_err.empty()) return g_err.c_str();
+    switch (code) {
+    case DCTQ_EINVAL: return "invalid argument";
+    case DCTQ_EHIP: return "HIP runtime error";
+    case DCTQ_ENOMEM: return "out of device memory";
+    case DCTQ_ENODEV: return "no gfx950 device";
+    default: return "unknown error";
+    }
+}
+
+/* Introspection for tests (host-only, no GPU needed): the tables a plan would use. */
+int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *dct, double *quant) {
+    double q[64];
+    quality = dctq_host::clamp_quality(quality);
+    dctq_host::quant_matrix(8, quality, q);
+    dctq::FastTables t;
+    dctq::fill_fast_tables(q, adaptive, &t);
+    if (w) memcpy(w, t.w, sizeof t.w);
+    if (thr) memcpy(thr, t.thr, sizeof t.thr);
+    if (dct) dctq_host::dct_matrix(8, dct);
+    if (quant) memcpy(quant, q, sizeof q);
+    return DCTQ_OK;
+}
+
+int dctq_debug_fastdiv(uint32_t d, uint32_t n) {
+    dctq::FastDiv f = dctq::make_fastdiv(d);
+    return (int)((((uint64_t)n * f.m >> 32) + n) >> f.s);
+}
+
+}  // extern "C"

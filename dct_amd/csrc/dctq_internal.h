@@ -1,0 +1,50 @@
+// dct_amd/csrc/dctq_internal.h -- shared between the kernels and the C-ABI shim.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dctq {
+
+// n / d and n % d by multiply-high, valid for 0 <= n < 2^31 (host-built magic).
+struct FastDiv {
+    uint32_t d, m, s;
+};
+FastDiv make_fastdiv(uint32_t d);
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (__umulhi(n, f.m) + n) >> f.s; }
+
+// Wave-uniform per-plan constants of the fp32 fast path, passed by value in the
+// kernel arguments so every access is a scalar load into SGPRs.
+struct FastTables {
+    float w[64];    // S_i S_j / Q_ij  (AAN output scale folded into 1/Q)
+    float thr[64];  // |frac| above which the exact fp64 path decides (guard band)
+};
+
+// Per-plan device-resident tables (runtime-indexed: exact tie path, inverse).
+struct DevTables {
+    double dct[64];    // D of src/dct.c:17-30, bit-identical to the host expression
+    double quant[64];  // Q of src/quantization.c:51-99
+    double dequant[64];// 1/Q (src/quantization.c:101-111)
+    double iscale[64]; // inverse path: 1/Q * S_i S_j (non-adaptive dequant folded with AAN^T scale)
+    double qscale[64]; // inverse path (adaptive): Q * S_i S_j
+    double s2[64];     // S_i S_j
+};
+
+struct PlaneArgs {
+    const uint8_t *src;
+    long long stride, frame_stride;
+    int bw;             // blocks per row
+    int nblk_frame;     // blocks per frame
+    int nblk;           // total blocks (all frames), < 2^31
+    FastDiv div_bw, div_frame;  // by bw and by nblk_frame
+};
+
+hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
+                              int16_t *coef, int32_t *var_num, unsigned long long *fallbacks,
+                              hipStream_t stream);
+hipError_t launch_fdct8_float(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);
+hipError_t launch_idct8(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
+                        long long nblk, float *recon, hipStream_t stream);
+hipError_t launch_synth(uint64_t seed, int kind, uint8_t *dst, long long stride, long long frame_stride,
+                        int width, int height, int nframes, hipStream_t stream);
+
+}  // namespace dctq

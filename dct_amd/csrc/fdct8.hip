@@ -1,0 +1,266 @@
+// dct_amd/csrc/fdct8.hip -- the MI355X hot path: 8x8 forward DCT + quantization.
+//
+// Replaces the per-block loop of the reference pipeline (tests/test_entropy.c:300-316):
+//   create_block_from_pixels (src/dct.c:109-120) -> dct_forward (src/dct.c:52-77)
+//   -> calculate_block_variance (src/quantization.c:153-169)
+//   -> quantize (src/quantization.c:113-131, adaptive :171-211)
+// for every block of a stack of u8 planes, in ONE launch.
+//
+// Layout (DESIGN.md "Kernels"): one LANE owns one 8x8 block, a wave64 owns 64
+// consecutive blocks in raster order.  Each lane loads its block as 8 x 8-byte
+// rows (a wave-instruction reads 512 contiguous bytes of one pixel row), runs the
+// separable AAN butterfly entirely in registers (no cross-lane traffic, all
+// constants wave-uniform), quantizes, and the wave stages its 8 KiB of int16
+// output through LDS so the global stores are 1 KiB contiguous per instruction.
+//
+// Exactness (DESIGN.md "Exactness"): the fp32 butterfly is ~1e-4 away from the
+// reference's fp64 values, which matters only when c/Q lies near a rounding
+// tie (x.5).  tools/guard_bound.py proves a per-coefficient error bound; a
+// coefficient whose fractional part is within that band of 0.5 is recomputed
+// by `exact_quant` in the reference's exact fp64 operation order (no FMA
+// contraction: this file is compiled with -ffp-contract=off), with IEEE
+// division and round-half-away-from-zero.  All other coefficients are provably
+// rounded the same way the reference rounds them.
+#include "dctq_internal.h"
+#include "fdct8_bound.h"
+
+namespace dctq {
+
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kPitch = 9;  // uint4 per block in the LDS stage: 128 B + 16 B pad
+constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23: fma(y, w, kMagic) rounds y*w to an integer in its low bits
+
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+
+// The 8-point AAN flow graph, operation for operation tools/aan_model.py::aan8
+// (the model tools/guard_bound.py bounds).  Outputs y_k with X_k = kAanScale[k]*y_k.
+template <typename T>
+__device__ __forceinline__ void aan8(T &v0, T &v1, T &v2, T &v3, T &v4, T &v5, T &v6, T &v7, T c4, T c6,
+                                     T c2mc6, T c2pc6) {
+    T a0 = v0 + v7, b0 = v0 - v7;
+    T a1 = v1 + v6, b1 = v1 - v6;
+    T a2 = v2 + v5, b2 = v2 - v5;
+    T a3 = v3 + v4, b3 = v3 - v4;
+    T e0 = a0 + a3, e3 = a0 - a3;
+    T e1 = a1 + a2, e2 = a1 - a2;
+    T y0 = e0 + e1, y4 = e0 - e1;
+    T m = (e2 + e3) * c4;
+    T y2 = e3 + m, y6 = e3 - m;
+    T o0 = b3 + b2;
+    T o1 = b2 + b1;
+    T o2 = b1 + b0;
+    T z5 = (o0 - o2) * c6;
+    T z2 = fma_t(c2mc6, o0, z5);
+    T z4 = fma_t(c2pc6, o2, z5);
+    T z3 = o1 * c4;
+    T z11 = b0 + z3, z13 = b0 - z3;
+    v0 = y0;
+    v1 = z11 + z4;
+    v2 = y2;
+    v3 = z13 - z2;
+    v4 = y4;
+    v5 = z13 + z2;
+    v6 = y6;
+    v7 = z11 - z4;
+}
+
+template <typename T>
+__device__ __forceinline__ void aan8x8(T (&v)[8][8], T c4, T c6, T c2mc6, T c2pc6) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) aan8(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7], c4, c6, c2mc6, c2pc6);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) aan8(v[0][c], v[1][c], v[2][c], v[3][c], v[4][c], v[5][c], v[6][c], v[7][c], c4, c6, c2mc6, c2pc6);
+}
+
+// Locate the lane's block: n -> (frame, by, bx) -> pointer to its top-left pixel.
+__device__ __forceinline__ const uint8_t *block_ptr(const PlaneArgs &p, uint32_t n) {
+    uint32_t f = fdiv(n, p.div_frame);
+    uint32_t rem = n - f * (uint32_t)p.nblk_frame;
+    uint32_t by = fdiv(rem, p.div_bw);
+    uint32_t bx = rem - by * (uint32_t)p.bw;
+    return p.src + (long long)f * p.frame_stride + (long long)(by * 8) * p.stride + (long long)bx * 8;
+}
+
+// Reference-order fp64 recomputation of ONE quantized coefficient c = 8i + j:
+//   temp[k][j] = sum_l x[k][l] * D^T[l][j]      (src/dct.c:57-64, l ascending)
+//   out[i][j]  = sum_k D[i][k] * temp[k][j]     (src/dct.c:67-74, k ascending)
+//   q          = (int) round(out / M_ij)        (src/quantization.c:124)
+// with x = (double)px - 128.0 (src/dct.c:115).  Separate multiply and add
+// (file compiled with -ffp-contract=off), each accumulator starting at 0.0.
+__device__ __noinline__ int exact_quant(const uint8_t *__restrict__ px, long long stride, int c,
+                                        const double *__restrict__ dct, double m) {
+    const int i = c >> 3, j = c & 7;
+    double out = 0.0;
+    for (int k = 0; k < 8; ++k) {
+        const uint2 row = *reinterpret_cast<const uint2 *>(px + k * stride);
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const uint32_t w = l < 4 ? row.x : row.y;
+            const double x = (double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0;
+            t += x * dct[j * 8 + l];
+        }
+        out += dct[i * 8 + k] * t;
+    }
+    return (int)round(out / m);
+}
+
+// src/quantization.c:171-211 for is_quantize=1, element c, given the block's
+// exact variance (var_num / 4096): nv = fmin(1, fmax(0.1, var/1000)),
+// M = Q*(2-nv) clamped to >= 1, DC keeps Q.
+__device__ __forceinline__ double adaptive_scale(int32_t var_num) {
+    const double var = (double)var_num / 4096.0;  // == (sum_sq/64) - mean*mean exactly
+    const double nv = fmin(1.0, fmax(0.1, var / 1000.0));
+    return 2.0 - nv;
+}
+
+template <bool ADAPTIVE, bool VAR, bool STATS>
+__global__ __launch_bounds__(kThreads) void fdct8_quant_kernel(PlaneArgs p, FastTables t,
+                                                               const DevTables *__restrict__ dev,
+                                                               int16_t *__restrict__ coef,
+                                                               int32_t *__restrict__ var_out,
+                                                               unsigned long long *fallbacks) {
+    __shared__ uint4 stage[kThreads * kPitch];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t wave0 = blockIdx.x * kThreads + wv * 64;  // first block of this wave
+    const uint32_t n = wave0 + lane;
+    const bool valid = n < (uint32_t)p.nblk;
+
+    // ---- load: 8 rows x 8 B per lane
+    const uint8_t *px = block_ptr(p, valid ? n : 0);
+    uint2 rows[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) rows[r] = *reinterpret_cast<const uint2 *>(px + r * p.stride);
+
+    // ---- unpack u8 -> fp32 (exact); the -128 centring is applied to Y00 only (exact)
+    float v[8][8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[r][k] = (float)((rows[r].x >> (8 * k)) & 0xFFu);
+            v[r][k + 4] = (float)((rows[r].y >> (8 * k)) & 0xFFu);
+        }
+
+    // ---- block variance numerator 64*sum(x^2) - sum(x)^2, x = px - 128 (exact integers)
+    int32_t var_num = 0;
+    if (ADAPTIVE || VAR) {
+        uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            s1 = __builtin_amdgcn_udot4(rows[r].x, 0x01010101u, s1, false);
+            s1 = __builtin_amdgcn_udot4(rows[r].y, 0x01010101u, s1, false);
+            s2 = __builtin_amdgcn_udot4(rows[r].x, rows[r].x, s2, false);
+            s2 = __builtin_amdgcn_udot4(rows[r].y, rows[r].y, s2, false);
+        }
+        const int32_t sx = (int32_t)s1 - 8192;
+        const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
+        var_num = 64 * sxx - sx * sx;
+        if (VAR && valid) var_out[n] = var_num;
+    }
+
+    // ---- 2-D butterfly
+    aan8x8(v, DCTQ_C4, DCTQ_C6, DCTQ_C2MC6, DCTQ_C2PC6);
+    v[0][0] -= 8192.0f;  // 64 * 128: exact (integer < 2^24)
+
+    float inv_s = 1.0f;
+    double s64 = 1.0;
+    if (ADAPTIVE) {
+        s64 = adaptive_scale(var_num);
+        inv_s = (float)(1.0 / s64);
+    }
+
+    // ---- quantize: t = rint(Y*w) in the low bits of t; flag |frac| beyond the guard
+    uint32_t packed[32];
+    uint32_t mlo = 0, mhi = 0;  // bit (31 - c%32) set => coefficient c needs the exact path
+#pragma unroll
+    for (int c = 0; c < 64; c += 2) {
+        uint32_t tb[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int cc = c + h;
+            const float y = v[cc >> 3][cc & 7];
+            const float w = (ADAPTIVE && cc != 0) ? t.w[cc] * inv_s : t.w[cc];
+            const float tt = __builtin_fmaf(y, w, kMagic);
+            const float r = tt - kMagic;
+            const float f = __builtin_fmaf(y, w, -r);
+            const uint32_t fl = fabsf(f) > t.thr[cc] ? 1u : 0u;
+            if (cc < 32) mlo = mlo + mlo + fl;
+            else mhi = mhi + mhi + fl;
+            tb[h] = __float_as_uint(tt);
+        }
+        packed[c >> 1] = __builtin_amdgcn_perm(tb[1], tb[0], 0x05040100u);
+    }
+
+    // ---- stage the lane's 128 B block in LDS (pitch 144 B: conflict-free b128 writes)
+    uint4 *mine = stage + (wv * 64 + lane) * kPitch;
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+        mine[s] = make_uint4(packed[4 * s], packed[4 * s + 1], packed[4 * s + 2], packed[4 * s + 3]);
+
+    // ---- rare path: exact fp64 reference-order recomputation of flagged coefficients
+    if (!valid) mlo = mhi = 0;
+    if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) {
+        int16_t *mine16 = reinterpret_cast<int16_t *>(mine);
+        int cnt = 0;
+        while (mlo | mhi) {
+            int c;
+            if (mlo) {
+                c = __clz(mlo);
+                mlo &= ~(0x80000000u >> c);
+            } else {
+                const int k = __clz(mhi);
+                mhi &= ~(0x80000000u >> k);
+                c = 32 + k;
+            }
+            double m = dev->quant[c];
+            if (ADAPTIVE && c != 0) {
+                m = m * s64;
+                if (m < 1.0) m = 1.0;
+            }
+            mine16[c] = (int16_t)exact_quant(px, p.stride, c, dev->dct, m);
+            ++cnt;
+        }
+        if (STATS) {
+            // wave-sum of cnt, one atomic per wave
+            int tot = cnt;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+            if (lane == 0 && tot) atomicAdd(fallbacks, (unsigned long long)tot);
+        }
+    }
+
+    // ---- wave-local LDS hand-off, then 1 KiB-contiguous global stores
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint4 *dst = reinterpret_cast<uint4 *>(coef) + (size_t)wave0 * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int m = k * 64 + lane;  // 16-byte chunk of the wave's 8 KiB output
+        const int bl = m >> 3;
+        if (wave0 + bl < (uint32_t)p.nblk) dst[m] = stage[(wv * 64 + bl) * kPitch + (m & 7)];
+    }
+}
+
+hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
+                              int16_t *coef, int32_t *var_num, unsigned long long *fallbacks,
+                              hipStream_t stream) {
+    const dim3 grid((p.nblk + kThreads - 1) / kThreads), block(kThreads);
+    const bool var = var_num != nullptr, stats = fallbacks != nullptr;
+#define DCTQ_LAUNCH(A, V, S) \
+    hipLaunchKernelGGL((fdct8_quant_kernel<A, V, S>), grid, block, 0, stream, p, t, dev, coef, var_num, fallbacks)
+    if (adaptive) {
+        if (var) { if (stats) DCTQ_LAUNCH(true, true, true); else DCTQ_LAUNCH(true, true, false); }
+        else { if (stats) DCTQ_LAUNCH(true, false, true); else DCTQ_LAUNCH(true, false, false); }
+    } else {
+        if (var) { if (stats) DCTQ_LAUNCH(false, true, true); else DCTQ_LAUNCH(false, true, false); }
+        else { if (stats) DCTQ_LAUNCH(false, false, true); else DCTQ_LAUNCH(false, false, false); }
+    }
+#undef DCTQ_LAUNCH
+    return hipGetLastError();
+}
+
+}  // namespace dctq

@@ -1,0 +1,77 @@
+/*
+ * host/frame_codec.c -- a plain C99 frame-level host of the batched C-ABI
+ * (include/dct_amd.h): generates a synthetic frame on the device, runs the
+ * forward DCT+quant hot path and the inverse, and prints a 64-bit FNV-1a
+ * checksum of the int16 coefficient plane plus the round-trip PSNR
+ * (tests/test_entropy.c:376-393 formula, clamped recon).
+ *
+ *   frame_codec WIDTH HEIGHT QUALITY ADAPTIVE SEED [KIND]
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "dct_amd.h"
+
+#define CHK(x)                                                                  \
+    do {                                                                        \
+        int rc_ = (x);                                                          \
+        if (rc_) {                                                              \
+            fprintf(stderr, "%s: %s\n", #x, dctq_error_string(rc_));            \
+            return 1;                                                           \
+        }                                                                       \
+    } while (0)
+
+int main(int argc, char **argv) {
+    if (argc < 6) {
+        fprintf(stderr, "usage: %s W H QUALITY ADAPTIVE SEED [KIND]\n", argv[0]);
+        return 2;
+    }
+    int w = atoi(argv[1]), h = atoi(argv[2]), q = atoi(argv[3]), ad = atoi(argv[4]);
+    uint64_t seed = strtoull(argv[5], NULL, 10);
+    int kind = argc > 6 ? atoi(argv[6]) : 0;
+    long long nblk = (long long)(w / 8) * (h / 8);
+    void *px, *coef, *var, *rec;
+    CHK(dctq_malloc(&px, (size_t)w * h));
+    CHK(dctq_malloc(&coef, (size_t)nblk * 128));
+    CHK(dctq_malloc(&var, (size_t)nblk * 4));
+    CHK(dctq_malloc(&rec, (size_t)nblk * 256));
+    dctq_plane pl = {(const uint8_t *)px, w, (long long)w * h, w, h, 1};
+    CHK(dctq_synth(seed, kind, &pl, NULL));
+    dctq_plan *plan;
+    CHK(dctq_plan_create(q, ad, &plan));
+    CHK(dctq_forward_quant(plan, &pl, (int16_t *)coef, (int32_t *)var, NULL));
+    CHK(dctq_inverse(plan, (const int16_t *)coef, (const int32_t *)var, nblk, (float *)rec, NULL));
+    CHK(dctq_synchronize(NULL));
+    int16_t *hc = malloc((size_t)nblk * 128);
+    float *hr = malloc((size_t)nblk * 256);
+    uint8_t *hp = malloc((size_t)w * h);
+    CHK(dctq_memcpy_dtoh(hc, coef, (size_t)nblk * 128));
+    CHK(dctq_memcpy_dtoh(hr, rec, (size_t)nblk * 256));
+    CHK(dctq_memcpy_dtoh(hp, px, (size_t)w * h));
+    uint64_t fnv = 1469598103934665603ULL;
+    const uint8_t *b = (const uint8_t *)hc;
+    for (long long i = 0; i < nblk * 128; ++i) fnv = (fnv ^ b[i]) * 1099511628211ULL;
+    double se = 0.0;
+    int bw = w / 8;
+    for (long long k = 0; k < nblk; ++k)
+        for (int e = 0; e < 64; ++e) {
+            int y = (int)(k / bw) * 8 + e / 8, x = (int)(k % bw) * 8 + e % 8;
+            double r = hr[k * 64 + e];
+            r = r < 0 ? 0 : r > 255 ? 255 : r;
+            double d = hp[(long long)y * w + x] - r;
+            se += d * d;
+        }
+    double mse = se / ((double)w * h);
+    printf("fnv1a:%016llx\n", (unsigned long long)fnv);
+    printf("psnr:%.4f\n", 10.0 * __builtin_log10(255.0 * 255.0 / mse));
+    dctq_plan_destroy(plan);
+    dctq_free(px);
+    dctq_free(coef);
+    dctq_free(var);
+    dctq_free(rec);
+    free(hc);
+    free(hr);
+    free(hp);
+    return 0;
+}

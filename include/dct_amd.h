@@ -1,0 +1,100 @@
+/*
+ * dct_amd.h -- batched (plane/frame-level) C-ABI of libdct_amd.so: the MI355X
+ * hot path.  New surface added NEXT TO the reference's per-block API
+ * (include/dct.h, include/quantization.h), which has no frame-level entry
+ * point: the reference's only frame-level caller is the per-block pipeline of
+ * tests/test_entropy.c:300-316 (create_block_from_pixels -> dct_forward ->
+ * calculate_block_variance -> quantize) and its inverse :350-373
+ * (dequantize -> dct_inverse).  Each entry point below replaces that loop over
+ * every 8x8 block of a plane with one HIP launch.
+ *
+ * Conventions: plain pointers and sizes, no HIP/torch types.  Device pointers
+ * are HIP device memory of the calling thread's current device; `stream` is a
+ * hipStream_t passed as void* (NULL = default stream).  Every call is
+ * asynchronous on `stream` and returns 0 or a negative DCTQ_E* code
+ * (dctq_error_string).  Results are bit-identical to the reference
+ * (src/dct.c + src/quantization.c) for the quantized path; see DESIGN.md.
+ */
+#ifndef DCT_AMD_H
+#define DCT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "quantization.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCTQ_OK 0
+#define DCTQ_EINVAL (-1)   /* bad argument (sizes not multiples of 8, misaligned, ...) */
+#define DCTQ_EHIP (-2)     /* a HIP runtime call failed (dctq_error_string has the detail) */
+#define DCTQ_ENOMEM (-3)
+#define DCTQ_ENODEV (-4)   /* no gfx950 device visible */
+
+/* Opaque per-configuration state: the host-computed tables (D of src/dct.c:17-30,
+ * Q of src/quantization.c:51-99, fast-path scale and guard tables) uploaded to
+ * the device that was current at creation. */
+typedef struct dctq_plan dctq_plan;
+
+/* quality is clamped to 1..100 exactly as quant_init does (src/quantization.c:26-31). */
+int dctq_plan_create(int quality, int adaptive, dctq_plan **plan);
+/* Bind an existing reference-style context (block_size must be 8); its
+ * quant_matrix VALUES are used, so a caller-modified table is honoured. */
+int dctq_plan_from_context(const QuantContext *qctx, dctq_plan **plan);
+void dctq_plan_destroy(dctq_plan *plan);
+
+/* A stack of equally-shaped u8 planes in device memory. */
+typedef struct {
+    const uint8_t *pixels;   /* frame 0, row 0; 8-byte aligned */
+    long long stride;        /* bytes between pixel rows; multiple of 8, >= width */
+    long long frame_stride;  /* bytes between consecutive frames */
+    int width, height;       /* multiples of 8 */
+    int nframes;             /* >= 1 */
+} dctq_plane;
+
+/* Forward DCT + quantization of every 8x8 block:
+ *   coef[f][by][bx][64] (int16, row-major within the block, blocks in raster
+ *   order -- the order the reference emits them) = quantize(dct_forward(px-128)).
+ * var_num (optional, may be NULL): per block 64*sum(x^2) - sum(x)^2 with
+ * x = px-128; calculate_block_variance() == var_num / 4096.0 exactly.  Needed by
+ * the adaptive inverse. */
+int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num,
+                       void *stream);
+
+/* Forward DCT only, float coefficients coef[f][by][bx][64]
+ * (|coef - dct_forward()| <= 1e-4; computed in fp64, rounded once to fp32). */
+int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream);
+
+/* Inverse: dequantize (reference semantics incl. the non-adaptive 1/Q
+ * multiplier, src/quantization.c:139,144) + dct_inverse + 128, per block:
+ *   recon[b][64] = dct_inverse(dequantize(coef[b], var_num[b]/4096)) + 128
+ * (float, unclamped; |err| <= 1e-4).  var_num is required when adaptive. */
+int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks,
+                 float *recon, void *stream);
+
+/* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented
+ * by the number of coefficients resolved by the exact fp64 tie path in later
+ * dctq_forward_quant calls on this plan (costs one atomic per affected wave). */
+int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter);
+
+/* Synthetic frames (counter-based splitmix64; identical to the oracle's
+ * generator): kind 0 uniform, 1 smooth, 2 constant 8x8 blocks, 3 extremes.
+ * Frame f uses seed + f. */
+int dctq_synth(uint64_t seed, int kind, const dctq_plane *dst, void *stream);
+
+/* Device helpers so a plain C host needs no HIP headers. */
+int dctq_device_count(int *count);
+int dctq_set_device(int device);
+int dctq_malloc(void **ptr, size_t bytes);
+int dctq_free(void *ptr);
+int dctq_memcpy_htod(void *dst, const void *src, size_t bytes);
+int dctq_memcpy_dtoh(void *dst, const void *src, size_t bytes);
+int dctq_synchronize(void *stream);
+const char *dctq_error_string(int code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

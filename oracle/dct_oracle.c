@@ -1,0 +1,322 @@
+/*
+ * oracle/dct_oracle.c -- TEST INFRASTRUCTURE ONLY (the parity checker / CPU baseline).
+ *
+ * A clean-room, flat-array CPU restatement of the reference hot path
+ * (erkinov-wtf/dct: src/dct.c + src/quantization.c) that follows the
+ * reference's floating-point operation ORDER exactly, so that its results are
+ * bit-identical to the reference's.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load this library.  The product (dct_amd/)
+ * never links or calls it.
+ *
+ * Pinned: tests/test_oracle.py checks every function below against golden
+ * vectors produced by the reference itself (compiled from /root/reference by
+ * oracle/Makefile into oracle/_ref/, fixtures in tests/golden/).
+ *
+ * Build: -std=c99 -O2 -ffp-contract=off (the reference's -std=c99 already
+ * implies no contraction under gcc; we make it explicit).
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "dct_oracle.h"
+
+/* include/dct.h:15 -- the literal the reference uses for pi. */
+#define ORC_PI 3.14159265358979323846
+
+/* src/quantization.c:8-17 -- JPEG Annex K luminance table. */
+static const int orc_luma[64] = {
+    16, 11, 10, 16, 24, 40, 51, 61,     12, 12, 14, 19, 26, 58, 60, 55,
+    14, 13, 16, 24, 40, 57, 69, 56,     14, 17, 22, 29, 51, 87, 80, 62,
+    18, 22, 37, 56, 68, 109, 103, 77,   24, 35, 55, 64, 81, 104, 113, 92,
+    49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+
+/* src/dct.c:17-30: D[i][j] = alpha_i * cos(PI*(2j+1)*i / (2N)).
+ * The expression is evaluated as in the reference: (PI*(2j+1))*i, then the
+ * quotient by (2.0*N); alpha_0 = 1/sqrt(N), alpha_i = sqrt(2/N). */
+void orc_dct_matrix(int n, double *d) {
+    for (int i = 0; i < n; ++i) {
+        double a = (i == 0) ? 1.0 / sqrt(n) : sqrt(2.0 / n);
+        for (int j = 0; j < n; ++j) d[i * n + j] = a * cos((ORC_PI * (2 * j + 1) * i) / (2.0 * n));
+    }
+}
+
+/* src/quantization.c:51-99 (scale factor :55-60; 8x8 JPEG table :63-77; radial
+ * formula for other sizes :80-96).  Quality is NOT clamped here (quant_init
+ * clamps, :26-31). */
+void orc_quant_matrix(int n, int quality, double *q) {
+    double s;
+    if (quality < 50)
+        s = 5000.0 / quality;
+    else
+        s = 200.0 - 2 * quality;
+    s /= 100.0;
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double v;
+            if (n == 8)
+                v = orc_luma[i * 8 + j] * s;
+            else
+                v = (1.0 + sqrt((double)(i * i + j * j))) * s * 8.0;
+            if (v < 1.0) v = 1.0;
+            if (v > 255.0) v = 255.0;
+            q[i * n + j] = v;
+        }
+}
+
+/* src/quantization.c:101-111: dequant = 1.0 / Q. */
+void orc_dequant_matrix(int n, const double *q, double *dq) {
+    for (int k = 0; k < n * n; ++k) dq[k] = 1.0 / q[k];
+}
+
+/* src/quantization.c:26-31 */
+int orc_clamp_quality(int quality) {
+    if (quality < 1) quality = 1;
+    if (quality > 100) quality = 100;
+    return quality;
+}
+
+/* src/dct.c:52-77: temp = X * D^T (k ascending), out = D * temp (k ascending),
+ * each accumulator starting at 0.0, separate multiply and add. */
+void orc_forward(int n, const double *d, const double *x, double *out) {
+    double tmp[64 * 64];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) acc += x[i * n + k] * d[j * n + k]; /* D^T[k][j] = D[j][k] */
+            tmp[i * n + j] = acc;
+        }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) acc += d[i * n + k] * tmp[k * n + j];
+            out[i * n + j] = acc;
+        }
+}
+
+/* src/dct.c:80-105: temp = D^T * C, out = temp * D. */
+void orc_inverse(int n, const double *d, const double *c, double *out) {
+    double tmp[64 * 64];
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) acc += d[k * n + i] * c[k * n + j]; /* D^T[i][k] = D[k][i] */
+            tmp[i * n + j] = acc;
+        }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) acc += tmp[i * n + k] * d[k * n + j];
+            out[i * n + j] = acc;
+        }
+}
+
+/* src/quantization.c:153-169: row-major sum / sum of squares, mean = sum/count,
+ * var = sum_sq/count - mean^2. */
+double orc_variance(int n, const double *x) {
+    double s = 0.0, s2 = 0.0;
+    int cnt = n * n;
+    for (int k = 0; k < cnt; ++k) {
+        s += x[k];
+        s2 += x[k] * x[k];
+    }
+    double mean = s / cnt;
+    return (s2 / cnt) - (mean * mean);
+}
+
+/* src/quantization.c:171-211: per-block matrix.  nv = fmin(1, fmax(0.1, var/1000));
+ * quantize: src=Q, scale = 2-nv, clamp >= 1; dequantize: src=1/Q, scale = 1/(2-nv).
+ * Element (0,0) keeps the source value. */
+void orc_adjust(int n, const double *src, double variance, int is_quantize, double *m) {
+    double nv = fmin(1.0, fmax(0.1, variance / 1000.0));
+    double scale = is_quantize ? 2.0 - nv : 1.0 / (2.0 - nv);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double v;
+            if (i == 0 && j == 0) {
+                v = src[0];
+            } else {
+                v = src[i * n + j] * scale;
+                if (is_quantize && v < 1.0) v = 1.0;
+            }
+            m[i * n + j] = v;
+        }
+}
+
+/* src/quantization.c:113-131: q = (int) round(c / M). */
+void orc_quantize(int n, const double *qm, int adaptive, double variance, const double *c, int *q) {
+    double adj[64 * 64];
+    const double *m = qm;
+    if (adaptive) {
+        orc_adjust(n, qm, variance, 1, adj);
+        m = adj;
+    }
+    for (int k = 0; k < n * n; ++k) q[k] = (int)round(c[k] / m[k]);
+}
+
+/* src/quantization.c:133-151: non-adaptive dq = q * (1/Q) (the reference's
+ * dequant table -- bug-compatible); adaptive dq = q * (1.0 / M)
+ * with M = adjust(1/Q, var, 0). */
+void orc_dequantize(int n, const double *dqm, int adaptive, double variance, const int *q, double *c) {
+    double adj[64 * 64];
+    if (adaptive) {
+        orc_adjust(n, dqm, variance, 0, adj);
+        for (int k = 0; k < n * n; ++k) c[k] = q[k] * (1.0 / adj[k]);
+    } else {
+        for (int k = 0; k < n * n; ++k) c[k] = q[k] * dqm[k];
+    }
+}
+
+/* src/dct.c:109-120: x = (double)pixel - 128.0 from a row-major plane. */
+void orc_block_from_pixels(const uint8_t *px, long stride, int row0, int col0, int n, double *x) {
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) x[i * n + j] = (double)px[(long)(row0 + i) * stride + (col0 + j)] - 128.0;
+}
+
+/* ---------------------------------------------------------------------------
+ * Plane drivers: the per-block pipeline of tests/test_entropy.c:300-316
+ * (pixels-128 -> dct_forward -> variance -> quantize) applied to every 8x8 block
+ * of a plane in raster order; blocks are emitted as [by][bx][8][8] int16.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+    const uint8_t *px;
+    long stride;
+    int bw, bh, quality, adaptive;
+    int16_t *out;
+    double *fout; /* optional float-coefficient output [nblk][64] */
+    int row_lo, row_hi;
+    double d[64], q[64];
+} orc_job;
+
+static void orc_rows(orc_job *jb) {
+    double x[64], c[64];
+    int qi[64];
+    for (int by = jb->row_lo; by < jb->row_hi; ++by)
+        for (int bx = 0; bx < jb->bw; ++bx) {
+            long b = (long)by * jb->bw + bx;
+            orc_block_from_pixels(jb->px, jb->stride, by * 8, bx * 8, 8, x);
+            orc_forward(8, jb->d, x, c);
+            if (jb->fout) memcpy(jb->fout + b * 64, c, sizeof c);
+            if (jb->out) {
+                double var = jb->adaptive ? orc_variance(8, x) : 0.0;
+                orc_quantize(8, jb->q, jb->adaptive, var, c, qi);
+                for (int k = 0; k < 64; ++k) jb->out[b * 64 + k] = (int16_t)qi[k];
+            }
+        }
+}
+
+static void *orc_thread(void *arg) {
+    orc_rows((orc_job *)arg);
+    return NULL;
+}
+
+int orc_forward_plane(const uint8_t *px, long stride, int width, int height, int quality, int adaptive,
+                      int16_t *out, double *fout, int nthreads) {
+    if (width % 8 || height % 8 || nthreads < 1) return -1;
+    int bw = width / 8, bh = height / 8;
+    if (nthreads > bh) nthreads = bh > 0 ? bh : 1;
+    orc_job *jobs = calloc((size_t)nthreads, sizeof *jobs);
+    pthread_t *th = calloc((size_t)nthreads, sizeof *th);
+    if (!jobs || !th) return -2;
+    for (int t = 0; t < nthreads; ++t) {
+        orc_job *jb = &jobs[t];
+        jb->px = px;
+        jb->stride = stride;
+        jb->bw = bw;
+        jb->bh = bh;
+        jb->quality = orc_clamp_quality(quality);
+        jb->adaptive = adaptive;
+        jb->out = out;
+        jb->fout = fout;
+        jb->row_lo = (int)((long)bh * t / nthreads);
+        jb->row_hi = (int)((long)bh * (t + 1) / nthreads);
+        orc_dct_matrix(8, jb->d);
+        orc_quant_matrix(8, jb->quality, jb->q);
+    }
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, orc_thread, &jobs[t]);
+    orc_rows(&jobs[0]);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    free(jobs);
+    free(th);
+    return 0;
+}
+
+/* Inverse pipeline of tests/test_entropy.c:350-393 per block:
+ * dequantize(q, var) -> dct_inverse -> recon = out + 128 (double, unclamped).
+ * `var` per block is needed for adaptive mode (the forward pass's variance). */
+int orc_inverse_plane(const int16_t *coef, const double *var, int nblocks, int quality, int adaptive,
+                      double *recon) {
+    double d[64], q[64], dq[64], c[64], o[64];
+    int qi[64];
+    orc_dct_matrix(8, d);
+    orc_quant_matrix(8, orc_clamp_quality(quality), q);
+    orc_dequant_matrix(8, q, dq);
+    for (long b = 0; b < nblocks; ++b) {
+        for (int k = 0; k < 64; ++k) qi[k] = coef[b * 64 + k];
+        orc_dequantize(8, dq, adaptive, var ? var[b] : 0.0, qi, c);
+        orc_inverse(8, d, c, o);
+        for (int k = 0; k < 64; ++k) recon[b * 64 + k] = o[k];
+    }
+    return 0;
+}
+
+/* Per-block variance of a plane (adaptive side-channel for the inverse). */
+int orc_plane_variance(const uint8_t *px, long stride, int width, int height, double *var) {
+    double x[64];
+    int bw = width / 8, bh = height / 8;
+    for (int by = 0; by < bh; ++by)
+        for (int bx = 0; bx < bw; ++bx) {
+            orc_block_from_pixels(px, stride, by * 8, bx * 8, 8, x);
+            var[(long)by * bw + bx] = orc_variance(8, x);
+        }
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * Synthetic frames.  A counter-based splitmix64 (Steele et al. 2014) so that the
+ * host, the tests and the device generator (dct_amd/csrc/synth.hip) agree bit
+ * for bit without shipping data.  All arithmetic is integer.
+ * ------------------------------------------------------------------------- */
+static uint64_t orc_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+uint64_t orc_splitmix(uint64_t seed, uint64_t i) { return orc_mix(seed + (i + 1) * 0x9E3779B97F4A7C15ULL); }
+
+/* kind: 0 uniform, 1 smooth (bilinear random lattice + small noise),
+ *       2 constant 8x8 blocks, 3 extremes (each pixel 0 or 255) */
+uint8_t orc_synth_pixel(uint64_t seed, int kind, int width, int x, int y) {
+    uint64_t idx = (uint64_t)y * (uint64_t)width + (uint64_t)x;
+    switch (kind) {
+    case 0:
+        return (uint8_t)(orc_splitmix(seed, idx) & 0xFF);
+    case 1: {
+        int cx = x >> 4, cy = y >> 4, fx = x & 15, fy = y & 15;
+        uint64_t s2 = seed ^ 0x5DEECE66DULL;
+        int gw = (width >> 4) + 2;
+        int v00 = (int)(orc_splitmix(s2, (uint64_t)cy * gw + cx) & 0xFF);
+        int v01 = (int)(orc_splitmix(s2, (uint64_t)cy * gw + cx + 1) & 0xFF);
+        int v10 = (int)(orc_splitmix(s2, (uint64_t)(cy + 1) * gw + cx) & 0xFF);
+        int v11 = (int)(orc_splitmix(s2, (uint64_t)(cy + 1) * gw + cx + 1) & 0xFF);
+        int top = v00 * (16 - fx) + v01 * fx, bot = v10 * (16 - fx) + v11 * fx;
+        int v = (top * (16 - fy) + bot * fy + 128) >> 8;
+        int noise = (int)(orc_splitmix(seed, idx) & 7) - 3;
+        v += noise;
+        return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+    }
+    case 2: {
+        uint64_t b = (uint64_t)(y >> 3) * (uint64_t)((width + 7) >> 3) + (uint64_t)(x >> 3);
+        return (uint8_t)(orc_splitmix(seed, b) & 0xFF);
+    }
+    default:
+        return (orc_splitmix(seed, idx) & 1) ? 255 : 0;
+    }
+}
+
+void orc_synth_plane(uint64_t seed, int kind, int width, int height, uint8_t *px, long stride) {
+    for (int y = 0; y < height; ++y)
+        for (int x = 0; x < width; ++x) px[(long)y * stride + x] = orc_synth_pixel(seed, kind, width, x, y);
+}

@@ -1,0 +1,356 @@
+"""GPU parity: the HIP path (through the C-ABI of libdct_amd.so) against the
+oracle and the reference's golden vectors.  Integer outputs must be bit-exact;
+float outputs within 1e-4 (BASELINE.json north_star)."""
+import ctypes as C
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import f64
+
+pytestmark = pytest.mark.gpu
+
+QUALITIES = [1, 10, 25, 50, 75, 90, 100]
+
+
+@pytest.fixture(scope="module")
+def T():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    import dct_amd
+    dct_amd.lib()
+    return torch
+
+
+@pytest.fixture(scope="module")
+def dm(T):
+    import dct_amd
+    return dct_amd
+
+
+def gpu_px(T, px):
+    return T.from_numpy(np.ascontiguousarray(px)).cuda()
+
+
+def test_synth_matches_oracle(T, dm):
+    import oracle as O
+    for kind, k in O.KINDS.items():
+        for (w, h) in [(128, 128), (40, 24), (1920, 1080)]:
+            g = dm.synth(777, kind, w, h).cpu().numpy()[0]
+            assert np.array_equal(g, O.synth_plane(777, k, w, h)), (kind, w, h)
+
+
+def test_forward_quant_tiles_bit_exact(T, dm, tiles):
+    """128x128 tiles of every synthetic kind vs the REFERENCE's own quantized output."""
+    for kind in ["uniform", "smooth", "const", "extreme"]:
+        px = tiles[f"{kind}_px"]
+        g = gpu_px(T, px)
+        for q in QUALITIES:
+            for ad in (0, 1):
+                out = dm.Plan(q, ad).forward_quant(g).cpu().numpy()
+                want = tiles[f"{kind}_q{q}_a{ad}"]
+                bad = np.argwhere(out != want)
+                assert bad.size == 0, f"{kind} q{q} a{ad}: {len(bad)} mismatches, first {bad[:4].tolist()}"
+
+
+def test_forward_quant_full_size_digests(T, dm, digests):
+    """BASELINE sizes (4K luma, 4K 4:2:0 chroma, 512^2): sha256 of the int16 planes
+    equals the reference's, frames regenerated on the device from the seed."""
+    seed = digests["seed"]
+    for e in digests["entries"]:
+        px = dm.synth(seed, e["kind"], e["width"], e["height"])
+        out = dm.Plan(e["quality"], e["adaptive"]).forward_quant(px).cpu().numpy()
+        got = hashlib.sha256(out.tobytes()).hexdigest()
+        assert got == e["sha256"], e
+
+
+def test_forward_quant_vs_oracle_many_seeds(T, dm):
+    import oracle as O
+    rng = np.random.default_rng(5)
+    for trial in range(12):
+        kind = ["uniform", "smooth", "const", "extreme"][trial % 4]
+        q = int(rng.integers(1, 101))
+        ad = int(trial % 3 == 0)
+        w, h = 8 * int(rng.integers(1, 90)), 8 * int(rng.integers(1, 40))
+        px = O.synth_plane(1000 + trial, O.KINDS[kind], w, h)
+        got = dm.Plan(q, ad).forward_quant(gpu_px(T, px)).cpu().numpy()
+        want = O.forward_plane(px, q, ad)
+        assert np.array_equal(got, want), (kind, q, ad, w, h, int((got != want).sum()))
+
+
+def test_quality_sweep_adversarial(T, dm):
+    """Every quality 1..100, both modes, on inputs built to hit rounding ties:
+    constant blocks (DC = 8*(p-128)), two-level stripes and checkerboards."""
+    import oracle as O
+    rng = np.random.default_rng(11)
+    blocks = []
+    for v in range(256):
+        blocks.append(np.full((8, 8), v, np.uint8))
+    for _ in range(128):
+        a, b = rng.integers(0, 256, 2)
+        m = np.indices((8, 8)).sum(0) % 2 == 0
+        blocks.append(np.where(m, a, b).astype(np.uint8))
+        s = np.zeros((8, 8), np.uint8)
+        s[:, :4], s[:, 4:] = a, b
+        blocks.append(s)
+        blocks.append(s.T.copy())
+    blocks.append(np.zeros((8, 8), np.uint8))
+    blocks.append(np.full((8, 8), 255, np.uint8))
+    nb = len(blocks)
+    px = np.concatenate(blocks, axis=1)  # one block row, nb blocks wide
+    g = gpu_px(T, px)
+    for q in range(1, 101):
+        for ad in (0, 1):
+            got = dm.Plan(q, ad).forward_quant(g).cpu().numpy()
+            want = O.forward_plane(px, q, ad)
+            assert np.array_equal(got, want), (q, ad, int((got != want).sum()))
+    assert nb > 64
+
+
+def test_edge_geometries(T, dm):
+    """Block counts not multiple of the wave/workgroup size, single column/row,
+    padded row stride, multi-frame stacks with a frame gap."""
+    import torch
+    import oracle as O
+    for (w, h) in [(8, 8), (8, 64), (512, 8), (8 * 63, 8), (8 * 65, 8), (8 * 257, 8), (24, 16)]:
+        px = O.synth_plane(3, 0, w, h)
+        got = dm.Plan(50, 0).forward_quant(gpu_px(T, px)).cpu().numpy()
+        assert np.array_equal(got, O.forward_plane(px, 50, 0)), (w, h)
+    # padded stride + frame gap: [F, H, Wpad] buffer, view [:, :, :W]
+    F, H, W, Wp = 3, 40, 56, 72
+    big = torch.zeros((F, H + 2, Wp), dtype=torch.uint8, device="cuda")
+    ref = []
+    for f in range(F):
+        p = O.synth_plane(40 + f, f % 4, W, H)
+        big[f, :H, :W] = torch.from_numpy(p).cuda()
+        ref.append(O.forward_plane(p, 75, 1))
+    view = big[:, :H, :W]
+    got = dm.Plan(75, 1).forward_quant(view).cpu().numpy()
+    assert np.array_equal(got, np.concatenate(ref))
+
+
+def test_var_num_exact(T, dm, tiles):
+    import oracle as O
+    for kind in ["uniform", "smooth", "const"]:
+        px = tiles[f"{kind}_px"]
+        vn = T.zeros(px.size // 64, dtype=T.int32, device="cuda")
+        dm.Plan(50, 1).forward_quant(gpu_px(T, px), var_num=vn)
+        var = vn.cpu().numpy().astype(np.float64) / 4096.0
+        assert np.array_equal(var, O.plane_variance(px)), kind
+
+
+def test_fallback_counter_and_exactness(T, dm):
+    """Constant blocks at q50 tie at DC in half of the blocks: the exact path runs."""
+    import oracle as O
+    px = O.synth_plane(9, 2, 1024, 512)
+    cnt = T.zeros(1, dtype=T.int64, device="cuda")
+    plan = dm.Plan(50, 0)
+    plan.set_fallback_counter(cnt)
+    got = plan.forward_quant(gpu_px(T, px)).cpu().numpy()
+    plan.set_fallback_counter(None)
+    assert np.array_equal(got, O.forward_plane(px, 50, 0))
+    n = int(cnt.item())
+    nblk = px.size // 64
+    assert 0.3 * nblk < n < 0.7 * nblk, n
+
+
+def test_forward_float_tolerance(T, dm, tiles):
+    import oracle as O
+    for kind in ["uniform", "smooth", "const", "extreme"]:
+        px = tiles[f"{kind}_px"]
+        got = dm.Plan(50, 0).forward_float(gpu_px(T, px)).cpu().numpy().astype(np.float64)
+        assert np.abs(got[:32] - tiles[f"{kind}_forward32"]).max() <= 1e-4, kind
+        _, want = O.forward_plane(px, 50, 0, want_float=True)
+        assert np.abs(got - want).max() <= 1e-4, kind
+
+
+def test_inverse_round_trip(T, dm):
+    import oracle as O
+    for kind in ["uniform", "smooth"]:
+        px = O.synth_plane(21, O.KINDS[kind], 256, 128)
+        for q, ad in [(50, 0), (50, 1), (90, 0), (10, 1), (100, 0)]:
+            plan = dm.Plan(q, ad)
+            vn = T.zeros(px.size // 64, dtype=T.int32, device="cuda")
+            coef = plan.forward_quant(gpu_px(T, px), var_num=vn)
+            rec = plan.inverse(coef, var_num=vn).cpu().numpy().astype(np.float64)
+            want = O.inverse_plane(coef.cpu().numpy(), q, ad, O.plane_variance(px) if ad else None) + 128.0
+            assert np.abs(rec - want).max() <= 1e-4, (kind, q, ad, np.abs(rec - want).max())
+
+
+def test_example_block_pipeline(T, dm, blocks):
+    """tests/test_entropy.c:290-393 example block through the batched API."""
+    from golden.make_golden import EXAMPLE
+    px = EXAMPLE.reshape(8, 8)
+    for q in QUALITIES:
+        for ad in (0, 1):
+            plan = dm.Plan(q, ad)
+            vn = T.zeros(1, dtype=T.int32, device="cuda")
+            coef = plan.forward_quant(gpu_px(T, px), var_num=vn)
+            assert coef.cpu().numpy().ravel().tolist() == blocks[f"example_q{q}_a{ad}"]
+            rec = plan.inverse(coef, var_num=vn).cpu().numpy().astype(np.float64).ravel()
+            want = f64(blocks[f"example_recon{q}_a{ad}"]) + 128.0
+            assert np.abs(rec - want).max() <= 1e-4
+    got = dm.Plan(50, 0).forward_float(gpu_px(T, px)).cpu().numpy().ravel()
+    assert np.abs(got - f64(blocks["example_forward"])).max() <= 1e-4
+
+
+def test_invalid_arguments(T, dm):
+    import torch
+    plan = dm.Plan(50, 0)
+    with pytest.raises(dm.DctqError):
+        plan.forward_quant(torch.zeros((12, 16), dtype=torch.uint8, device="cuda"))
+    with pytest.raises(dm.DctqError):
+        plan.forward_quant(torch.zeros((16, 16), dtype=torch.uint8, device="cuda")[:, 1:9])
+    with pytest.raises(dm.DctqError):
+        dm.Plan(50, 1).inverse(torch.zeros((4, 64), dtype=torch.int16, device="cuda"))
+
+
+# ------------------------------------------------------------ legacy per-block API
+class DCTContext(C.Structure):
+    _fields_ = [("block_size", C.c_int), ("dct_matrix", C.POINTER(C.POINTER(C.c_double))),
+                ("transposed_dct", C.POINTER(C.POINTER(C.c_double)))]
+
+
+class QuantContext(C.Structure):
+    _fields_ = [("block_size", C.c_int), ("quality", C.c_int), ("quant_matrix", C.POINTER(C.POINTER(C.c_double))),
+                ("dequant_matrix", C.POINTER(C.POINTER(C.c_double))), ("adaptive", C.c_int)]
+
+
+@pytest.fixture(scope="module")
+def L(T, dm):
+    lib = dm.lib()
+    P2 = C.POINTER(C.POINTER(C.c_double))
+    I2 = C.POINTER(C.POINTER(C.c_int))
+    lib.dct_init.restype = C.POINTER(DCTContext)
+    lib.dct_forward.argtypes = [C.POINTER(DCTContext), P2, P2]
+    lib.dct_inverse.argtypes = [C.POINTER(DCTContext), P2, P2]
+    lib.alloc_array.restype = P2
+    lib.alloc_int_array.restype = I2
+    lib.free_array.argtypes = [P2, C.c_int]
+    lib.free_int_array.argtypes = [I2, C.c_int]
+    lib.quant_init.restype = C.POINTER(QuantContext)
+    lib.quantize.argtypes = [C.POINTER(QuantContext), P2, I2, C.c_double]
+    lib.dequantize.argtypes = [C.POINTER(QuantContext), I2, P2, C.c_double]
+    lib.calculate_block_variance.argtypes = [P2, C.c_int]
+    lib.calculate_block_variance.restype = C.c_double
+    lib.adjust_matrix_for_block.argtypes = [C.POINTER(QuantContext), C.c_double, C.c_int]
+    lib.adjust_matrix_for_block.restype = P2
+    lib.copy_block_to_coefficients.argtypes = [P2, I2, C.c_int]
+    lib.create_block_from_pixels.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.create_block_from_pixels.restype = P2
+    lib.dct_free.argtypes = [C.POINTER(DCTContext)]
+    lib.quant_free.argtypes = [C.POINTER(QuantContext)]
+    return lib
+
+
+def _put(L, a):
+    n = a.shape[0]
+    m = L.alloc_array(n, n)
+    for i in range(n):
+        for j in range(n):
+            m[i][j] = float(a[i, j])
+    return m
+
+
+def _get(m, n):
+    return np.array([[m[i][j] for j in range(n)] for i in range(n)])
+
+
+def _put_i(L, a):
+    n = a.shape[0]
+    m = L.alloc_int_array(n, n)
+    for i in range(n):
+        for j in range(n):
+            m[i][j] = int(a[i, j])
+    return m
+
+
+def _get_i(m, n):
+    return np.array([[m[i][j] for j in range(n)] for i in range(n)], np.int64)
+
+
+def test_legacy_transforms_bit_exact(L, blocks):
+    from golden.make_golden import EXAMPLE
+    ctx = L.dct_init(8)
+    assert (_get(ctx.contents.dct_matrix, 8).ravel().view(np.uint64) == np.array(blocks["dct8"], np.uint64)).all()
+    x = EXAMPLE.reshape(8, 8).astype(np.float64) - 128.0
+    a, b = _put(L, x), L.alloc_array(8, 8)
+    L.dct_forward(ctx, a, b)
+    got = _get(b, 8).ravel()
+    assert (got.view(np.uint64) == np.array(blocks["example_forward"], np.uint64)).all()
+    c = L.alloc_array(8, 8)
+    L.dct_inverse(ctx, b, c)
+    assert (_get(c, 8).ravel().view(np.uint64) == np.array(blocks["example_inverse_of_forward"], np.uint64)).all()
+    for m in (a, b, c):
+        L.free_array(m, 8)
+    L.dct_free(ctx)
+    for n in (4, 16):
+        ctx = L.dct_init(n)
+        xin = np.array(blocks[f"blk{n}_in"], np.float64).reshape(n, n)
+        a, b = _put(L, xin), L.alloc_array(n, n)
+        L.dct_forward(ctx, a, b)
+        assert (_get(b, n).ravel().view(np.uint64) == np.array(blocks[f"blk{n}_forward"], np.uint64)).all()
+        L.dct_inverse(ctx, a, b)
+        assert (_get(b, n).ravel().view(np.uint64) == np.array(blocks[f"blk{n}_inverse"], np.uint64)).all()
+        L.free_array(a, n)
+        L.free_array(b, n)
+        L.dct_free(ctx)
+
+
+def test_legacy_quantization_bit_exact(L, blocks):
+    from golden.make_golden import EXAMPLE
+    c = f64(blocks["example_forward"]).reshape(8, 8)
+    var = blocks["example_variance"]
+    px = (C.c_char * 64).from_buffer_copy(EXAMPLE.tobytes())
+    blk = L.create_block_from_pixels(px, 8, 0, 0, 8)
+    assert L.calculate_block_variance(blk, 8) == var
+    for q in QUALITIES:
+        for ad in (0, 1):
+            ctx = L.quant_init(8, q, ad)
+            cm, qm = _put(L, c), L.alloc_int_array(8, 8)
+            L.quantize(ctx, cm, qm, var)
+            assert _get_i(qm, 8).ravel().tolist() == blocks[f"example_q{q}_a{ad}"]
+            dq = L.alloc_array(8, 8)
+            L.dequantize(ctx, qm, dq, var)
+            assert (_get(dq, 8).ravel().view(np.uint64) == np.array(blocks[f"example_dq{q}_a{ad}"], np.uint64)).all()
+            L.free_array(cm, 8)
+            L.free_array(dq, 8)
+            L.free_int_array(qm, 8)
+            L.quant_free(ctx)
+    ctx = L.quant_init(8, 50, 1)
+    for vv in (0.0, 8.02, 99.5, 500.0, 864.2, 1000.0, 5000.0):
+        for isq in (0, 1):
+            m = L.adjust_matrix_for_block(ctx, vv, isq)
+            assert (_get(m, 8).ravel().view(np.uint64) == np.array(blocks[f"adjust_50_{vv}_{isq}"], np.uint64)).all()
+            L.free_array(m, 8)
+    L.quant_free(ctx)
+    cm, im = _put(L, c), L.alloc_int_array(8, 8)
+    L.copy_block_to_coefficients(cm, im, 8)
+    assert _get_i(im, 8).ravel().tolist() == blocks["example_round"]
+
+
+def test_c_host_programs(T, dm, blocks, tmp_path):
+    """The C hosts in host/ (linked against libdct_amd.so through include/*.h)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run(["make", "-C", os.path.join(root, "host")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    r = subprocess.run([os.path.join(root, "host", "block_pipeline")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = dict(l.split(":", 1) for l in r.stdout.strip().splitlines() if ":" in l)
+    assert [int(v) for v in lines["q50"].split()] == blocks["example_q50_a0"]
+    assert [int(v) for v in lines["q90"].split()] == blocks["example_q90_a0"]
+    assert int(lines["forward_bits0"], 16) == blocks["example_forward"][0]
+    import oracle as O
+    for (w, h, q, ad, kind) in [(1920, 1080, 50, 0, 0), (640, 480, 90, 1, 1)]:
+        r = subprocess.run([os.path.join(root, "host", "frame_codec"), str(w), str(h), str(q), str(ad), "12345",
+                            str(kind)], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        got = dict(l.split(":", 1) for l in r.stdout.strip().splitlines())
+        want = O.forward_plane(O.synth_plane(12345, kind, w, h), q, ad).tobytes()
+        fnv = 1469598103934665603
+        for b in want:
+            fnv = ((fnv ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+        assert int(got["fnv1a"], 16) == fnv, (w, h, q, ad)

@@ -1,0 +1,34 @@
+#!/bin/bash
+# tools/gpu_session.sh STEP... -- run on the GPU box (via gpurun) from the repo root.
+# Each step runs under its own timeout; a crash/timeout (exit not in {0,1}) ends
+# the session immediately (no further GPU work in this call).
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/session.log
+  local s=$(date +%s)
+  timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - s ))s)" | tee -a $OUT/session.log
+  tail -5 $OUT/$name.log | sed 's/^/    /'
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    info) run info 60 bash -c "rocm-smi --showproductname --showclocks 2>&1 | head -40; nproc; lscpu | grep 'Model name'" ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    test) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
+    testall) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
+    bench) run bench 600 python bench.py ;;
+    benchq) run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu ;;
+    pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "session done"
