@@ -36,7 +36,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-ffp-contract=off", "-Wall", "-Wno-unused-command-line-argument",
+           "-ffp-contract=off", "-fno-slp-vectorize", "-Wall", "-Wno-unused-command-line-argument",
            "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", LIB + ".tmp"]
     if verbose:

@@ -7,6 +7,7 @@
 // launches the kernels of fdct8.hip / fdct8_aux.hip on the caller's stream.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -18,7 +19,7 @@
 #include "host_tables.h"
 
 struct dctq_plan {
-    int quality, adaptive, device;
+    int quality, adaptive, device, num_cus, variant;
     dctq::FastTables fast;       // thresholds for the mode in `adaptive`
     dctq::DevTables host;        // host copy of the device tables
     dctq::DevTables *dev;        // device copy
@@ -73,6 +74,10 @@ void fill_fast_tables(const double *q, int adaptive, FastTables *t) {
         if ((double)tf > thr) tf = nextafterf(tf, 0.0f);
         t->w[c] = wf;
         t->thr[c] = tf;
+        const double tt = (double)tf * (double)tf;  // exact
+        float t2 = (float)tt;
+        if ((double)t2 > tt) t2 = nextafterf(t2, 0.0f);
+        t->thr2[c] = t2;
     }
 }
 }  // namespace dctq
@@ -91,6 +96,9 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
     p->quality = quality;
     p->adaptive = adaptive ? 1 : 0;
     p->device = dev;
+    p->num_cus = prop.multiProcessorCount;
+    p->variant = 2;
+    if (const char *v = getenv("DCTQ_FDCT_VARIANT")) p->variant = atoi(v);
     p->fallbacks = nullptr;
     dctq_host::dct_matrix(8, p->host.dct);
     for (int c = 0; c < 64; ++c) {
@@ -102,6 +110,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
         p->host.qscale[c] = q[c] * s2;
     }
     dctq::fill_fast_tables(q, p->adaptive, &p->fast);
+    p->host.fast = p->fast;
     hipError_t e = hipMalloc(&p->dev, sizeof(dctq::DevTables));
     if (e != hipSuccess) {
         delete p;
@@ -175,7 +184,7 @@ int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *co
     int rc = plane_args(src, &a);
     if (rc) return rc;
     HIPCHK(dctq::launch_fdct8_quant(a, plan->fast, plan->dev, plan->adaptive, coef, var_num, plan->fallbacks,
-                                    (hipStream_t)stream),
+                                    (hipStream_t)stream, plan->variant, plan->num_cus),
            "fdct8_quant launch");
     return DCTQ_OK;
 }

@@ -17,6 +17,7 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (__umul
 struct FastTables {
     float w[64];    // S_i S_j / Q_ij  (AAN output scale folded into 1/Q)
     float thr[64];  // |frac| above which the exact fp64 path decides (guard band)
+    float thr2[64]; // thr^2 rounded down: flag iff thr2 - f*f < 0
 };
 
 // Per-plan device-resident tables (runtime-indexed: exact tie path, inverse).
@@ -27,6 +28,7 @@ struct DevTables {
     double iscale[64]; // inverse path: 1/Q * S_i S_j (non-adaptive dequant folded with AAN^T scale)
     double qscale[64]; // inverse path (adaptive): Q * S_i S_j
     double s2[64];     // S_i S_j
+    FastTables fast;   // device copy of the fast-path tables (v2 reads them per batch)
 };
 
 struct PlaneArgs {
@@ -40,7 +42,7 @@ struct PlaneArgs {
 
 hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
                               int16_t *coef, int32_t *var_num, unsigned long long *fallbacks,
-                              hipStream_t stream);
+                              hipStream_t stream, int variant, int num_cus);
 hipError_t launch_fdct8_float(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);
 hipError_t launch_idct8(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
                         long long nblk, float *recon, hipStream_t stream);

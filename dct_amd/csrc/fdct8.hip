@@ -89,10 +89,13 @@ __device__ __forceinline__ const uint8_t *block_ptr(const PlaneArgs &p, uint32_t
 //   q          = (int) round(out / M_ij)        (src/quantization.c:124)
 // with x = (double)px - 128.0 (src/dct.c:115).  Separate multiply and add
 // (file compiled with -ffp-contract=off), each accumulator starting at 0.0.
-__device__ __noinline__ int exact_quant(const uint8_t *__restrict__ px, long long stride, int c,
+__device__ __forceinline__ int exact_quant(const uint8_t *__restrict__ px, long long stride, int c,
                                         const double *__restrict__ dct, double m) {
     const int i = c >> 3, j = c & 7;
     double out = 0.0;
+    // rolled: one row (8 doubles) live at a time -- this path must not set the
+    // register allocation of the streaming loop around it
+#pragma unroll 1
     for (int k = 0; k < 8; ++k) {
         const uint2 row = *reinterpret_cast<const uint2 *>(px + k * stride);
         double t = 0.0;
@@ -117,7 +120,7 @@ __device__ __forceinline__ double adaptive_scale(int32_t var_num) {
 }
 
 template <bool ADAPTIVE, bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads) void fdct8_quant_kernel(PlaneArgs p, FastTables t,
+__global__ __launch_bounds__(kThreads) void fdct8_quant_v1(PlaneArgs p, FastTables t,
                                                                const DevTables *__restrict__ dev,
                                                                int16_t *__restrict__ coef,
                                                                int32_t *__restrict__ var_out,
@@ -245,22 +248,276 @@ __global__ __launch_bounds__(kThreads) void fdct8_quant_kernel(PlaneArgs p, Fast
     }
 }
 
-hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
-                              int16_t *coef, int32_t *var_num, unsigned long long *fallbacks,
-                              hipStream_t stream) {
-    const dim3 grid((p.nblk + kThreads - 1) / kThreads), block(kThreads);
-    const bool var = var_num != nullptr, stats = fallbacks != nullptr;
-#define DCTQ_LAUNCH(A, V, S) \
-    hipLaunchKernelGGL((fdct8_quant_kernel<A, V, S>), grid, block, 0, stream, p, t, dev, coef, var_num, fallbacks)
-    if (adaptive) {
-        if (var) { if (stats) DCTQ_LAUNCH(true, true, true); else DCTQ_LAUNCH(true, true, false); }
-        else { if (stats) DCTQ_LAUNCH(true, false, true); else DCTQ_LAUNCH(true, false, false); }
-    } else {
-        if (var) { if (stats) DCTQ_LAUNCH(false, true, true); else DCTQ_LAUNCH(false, true, false); }
-        else { if (stats) DCTQ_LAUNCH(false, false, true); else DCTQ_LAUNCH(false, false, false); }
+// ============================================================================
+// v2 (default): persistent grid-stride kernel, sized for the gfx950 VALU cost
+// model measured in profiles/r01/valu_issue_rates.md.
+//  * each wave walks 64-block batches b, b+W, b+2W, ... and prefetches the next
+//    batch's 8 rows into registers while it computes the current one;
+//  * u8 -> fp32 with v_cvt_f32_ubyteN (inline asm, so the compiler cannot turn
+//    the first butterfly stage into half-rate SDWA integer adds + converts);
+//  * quantization in packed fp32 (the per-plan tables sit in SGPR pairs, which
+//    v_pk_* ops read at no extra cost), tie flags as sign bits of thr^2 - f^2
+//    shifted into a per-lane 64-bit mask with v_alignbit;
+//  * flagged (block, coefficient) pairs go to a wave-local LDS queue and are
+//    recomputed exactly 64 at a time (every lane busy), then patched in HBM --
+//    instead of stalling the whole wave on one lane's fp64 work.
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int kQCap = 128;
+constexpr int kPitch2 = 136;  // bytes per block in the v2 stage: 2-way (free) conflicts for the b32 writes  // per-wave tie queue; holds < 64 between rounds + one round of <= 64
+
+template <int K>
+__device__ __forceinline__ float cvt_ubyte(uint32_t w) {
+    float f;
+    if constexpr (K == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(w));
+    else if constexpr (K == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(w));
+    else if constexpr (K == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(w));
+    else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(w));
+    return f;
+}
+
+__device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 (&rows)[8]) {
+    const uint8_t *px = block_ptr(p, n < (uint32_t)p.nblk ? n : 0);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) rows[r] = *reinterpret_cast<const uint2 *>(px + r * p.stride);
+}
+
+// Exact reference-order quantization of coefficient c of the block at px (one
+// queue entry): exact_quant() above plus, for adaptive plans, the block's exact
+// variance and adjusted divisor (src/quantization.c:153-211).
+template <bool ADAPTIVE>
+__device__ int exact_entry(const uint8_t *__restrict__ px, long long stride, int c, const DevTables *__restrict__ dev) {
+    double m = dev->quant[c];
+    if (ADAPTIVE && c != 0) {
+        uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint2 row = *reinterpret_cast<const uint2 *>(px + k * stride);
+            s1 = __builtin_amdgcn_udot4(row.x, 0x01010101u, s1, false);
+            s1 = __builtin_amdgcn_udot4(row.y, 0x01010101u, s1, false);
+            s2 = __builtin_amdgcn_udot4(row.x, row.x, s2, false);
+            s2 = __builtin_amdgcn_udot4(row.y, row.y, s2, false);
+        }
+        const int32_t sx = (int32_t)s1 - 8192;
+        const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
+        m = m * adaptive_scale(64 * sxx - sx * sx);
+        if (m < 1.0) m = 1.0;
     }
-#undef DCTQ_LAUNCH
+    return exact_quant(px, stride, c, dev->dct, m);
+}
+
+template <bool ADAPTIVE, bool STATS>
+__device__ __forceinline__ void drain_queue(const PlaneArgs &p, const DevTables *__restrict__ dev,
+                                            int16_t *__restrict__ coef, const uint32_t *q, int &qn, int lane,
+                                            unsigned long long *fallbacks) {
+    // the wave's own coefficient stores must land before their patches
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int take = qn < 64 ? qn : 64;
+    if (lane < take) {
+        const uint32_t e = q[qn - take + lane];
+        const uint32_t n = e >> 6;
+        const int c = (int)(e & 63u);
+        const int val = exact_entry<ADAPTIVE>(block_ptr(p, n), p.stride, c, dev);
+        coef[(size_t)n * 64 + c] = (int16_t)val;
+    }
+    qn -= take;
+    if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
+}
+
+template <bool ADAPTIVE, bool VAR, bool STATS>
+__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneArgs p, FastTables t,
+                                                           const DevTables *__restrict__ dev,
+                                                           int16_t *__restrict__ coef,
+                                                           int32_t *__restrict__ var_out,
+                                                           unsigned long long *fallbacks) {
+    __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ uint32_t queue[kWaves * kQCap];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t nbatch = ((uint32_t)p.nblk + 63u) >> 6;
+    const uint32_t step = gridDim.x * kWaves;
+    uint32_t *q = queue + wv * kQCap;
+    int qn = 0;
+    const f2 M2 = {kMagic, kMagic};
+
+    uint32_t b = blockIdx.x * kWaves + wv;
+    uint2 nxt[8];
+    if (b < nbatch) load_rows(p, b * 64 + lane, nxt);
+    for (; b < nbatch; b += step) {
+        uint2 cur[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+        const uint32_t n = b * 64 + lane;
+        const bool valid = n < (uint32_t)p.nblk;
+        if (b + step < nbatch) load_rows(p, (b + step) * 64 + lane, nxt);
+
+        float v[8][8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            v[r][0] = cvt_ubyte<0>(cur[r].x);
+            v[r][1] = cvt_ubyte<1>(cur[r].x);
+            v[r][2] = cvt_ubyte<2>(cur[r].x);
+            v[r][3] = cvt_ubyte<3>(cur[r].x);
+            v[r][4] = cvt_ubyte<0>(cur[r].y);
+            v[r][5] = cvt_ubyte<1>(cur[r].y);
+            v[r][6] = cvt_ubyte<2>(cur[r].y);
+            v[r][7] = cvt_ubyte<3>(cur[r].y);
+        }
+        int32_t var_num = 0;
+        if (ADAPTIVE || VAR) {
+            uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                s1 = __builtin_amdgcn_udot4(cur[r].x, 0x01010101u, s1, false);
+                s1 = __builtin_amdgcn_udot4(cur[r].y, 0x01010101u, s1, false);
+                s2 = __builtin_amdgcn_udot4(cur[r].x, cur[r].x, s2, false);
+                s2 = __builtin_amdgcn_udot4(cur[r].y, cur[r].y, s2, false);
+            }
+            const int32_t sx = (int32_t)s1 - 8192;
+            const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
+            var_num = 64 * sxx - sx * sx;
+            if (VAR && valid) var_out[n] = var_num;
+        }
+
+        // ---- row pass, then column pairs fused with quantization: Y(i, c0..c0+1) is
+        // quantized right after its two columns are transformed and the packed int16
+        // pair goes straight to the LDS stage, so only 16 of the 64 values of the
+        // second pass are ever live (the block itself stays in registers).
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            aan8(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7], DCTQ_C4, DCTQ_C6,
+                 DCTQ_C2MC6, DCTQ_C2PC6);
+
+        f2 sc2 = {1.0f, 1.0f};
+        if (ADAPTIVE) {
+            const float inv = (float)(1.0 / adaptive_scale(var_num));
+            sc2 = f2{inv, inv};
+        }
+        // Per-plan tables through an opaque per-iteration pointer: scalar loads
+        // stay inside the loop instead of being hoisted into 128 live SGPRs.
+        const FastTables *tp = &dev->fast;
+        asm volatile("" : "+s"(tp));
+        uint32_t mlo = 0, mhi = 0;  // bit (31 - p%32): processing slot p = 16*cp + 2*i + h flagged
+        uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
+#pragma unroll
+        for (int cp = 0; cp < 4; ++cp) {
+            const int c0 = 2 * cp;
+            aan8(v[0][c0], v[1][c0], v[2][c0], v[3][c0], v[4][c0], v[5][c0], v[6][c0], v[7][c0], DCTQ_C4, DCTQ_C6,
+                 DCTQ_C2MC6, DCTQ_C2PC6);
+            aan8(v[0][c0 + 1], v[1][c0 + 1], v[2][c0 + 1], v[3][c0 + 1], v[4][c0 + 1], v[5][c0 + 1], v[6][c0 + 1],
+                 v[7][c0 + 1], DCTQ_C4, DCTQ_C6, DCTQ_C2MC6, DCTQ_C2PC6);
+            if (cp == 0) v[0][0] -= 8192.0f;  // 64 * 128: exact (integer < 2^24)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int c = i * 8 + c0;
+                const f2 y = {v[i][c0], v[i][c0 + 1]};
+                f2 w = {tp->w[c], tp->w[c + 1]};
+                if (ADAPTIVE) {
+                    if (c == 0) w.y *= sc2.y;  // the DC keeps Q (src/quantization.c:198-199)
+                    else w *= sc2;
+                }
+                const f2 tt = __builtin_elementwise_fma(y, w, M2);
+                const f2 nr = M2 - tt;
+                const f2 f = __builtin_elementwise_fma(y, w, nr);
+                const f2 T = {tp->thr2[c], tp->thr2[c + 1]};
+                const f2 d = __builtin_elementwise_fma(-f, f, T);  // < 0  <=>  |f| beyond the guard
+                if (cp < 2) {
+                    mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.x), 31);
+                    mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.y), 31);
+                } else {
+                    mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.x), 31);
+                    mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.y), 31);
+                }
+                st32[i * 4 + cp] = __builtin_amdgcn_perm(__float_as_uint(tt.y), __float_as_uint(tt.x), 0x05040100u);
+            }
+            // Pin the flag mask here: otherwise LLVM sinks the 32 residual tests of
+            // this column pair to their only use (the queue phase, after the
+            // stores) and keeps every residual live across the stores.
+            asm volatile("" : "+v"(mlo), "+v"(mhi));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint4 *dst = reinterpret_cast<uint4 *>(coef) + (size_t)b * 64 * 8;
+        const uint2 *st64 = reinterpret_cast<const uint2 *>(stage) + wv * 64 * (kPitch2 / 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int m = k * 64 + lane;
+            const int bl = m >> 3;
+            const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
+            if (b * 64 + bl < (uint32_t)p.nblk) dst[m] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
+
+        // ---- defer flagged coefficients to the wave's queue (rare: ~1.5 per batch at q50)
+        if (!valid) mlo = mhi = 0;
+        uint64_t has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
+        while (has) {
+            if (qn > kQCap - 64) drain_queue<ADAPTIVE, STATS>(p, dev, coef, q, qn, lane, fallbacks);
+            if (mlo | mhi) {
+                int slot;
+                if (mlo) {
+                    slot = __clz(mlo);
+                    mlo &= ~(0x80000000u >> slot);
+                } else {
+                    const int k = __clz(mhi);
+                    mhi &= ~(0x80000000u >> k);
+                    slot = 32 + k;
+                }
+                // slot = 16*cp + 2*i + h  ->  coefficient 8*i + 2*cp + h
+                const int c = (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
+                const uint32_t pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
+                q[pos] = (n << 6) | (uint32_t)c;
+            }
+            qn += __builtin_popcountll(has);
+            has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
+        }
+        if (qn >= 64) drain_queue<ADAPTIVE, STATS>(p, dev, coef, q, qn, lane, fallbacks);
+    }
+    while (qn > 0) drain_queue<ADAPTIVE, STATS>(p, dev, coef, q, qn, lane, fallbacks);
+}
+
+#define DCTQ_SELECT(KERN, A, V, S, ...)                                          \
+    do {                                                                         \
+        if (A) {                                                                 \
+            if (V) { if (S) KERN<true, true, true> __VA_ARGS__; else KERN<true, true, false> __VA_ARGS__; } \
+            else { if (S) KERN<true, false, true> __VA_ARGS__; else KERN<true, false, false> __VA_ARGS__; } \
+        } else {                                                                 \
+            if (V) { if (S) KERN<false, true, true> __VA_ARGS__; else KERN<false, true, false> __VA_ARGS__; } \
+            else { if (S) KERN<false, false, true> __VA_ARGS__; else KERN<false, false, false> __VA_ARGS__; } \
+        }                                                                        \
+    } while (0)
+
+template <bool A, bool V, bool S>
+static hipError_t launch_v1(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int16_t *coef,
+                            int32_t *var_num, unsigned long long *fb, hipStream_t stream) {
+    hipLaunchKernelGGL((fdct8_quant_v1<A, V, S>), dim3((p.nblk + kThreads - 1) / kThreads), dim3(kThreads), 0, stream,
+                       p, t, dev, coef, var_num, fb);
     return hipGetLastError();
 }
 
+template <bool A, bool V, bool S>
+static hipError_t launch_v2(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int16_t *coef,
+                            int32_t *var_num, unsigned long long *fb, hipStream_t stream, int num_cus) {
+    static int per_cu = 0;  // resident workgroups per CU for this instantiation
+    if (per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fdct8_quant_v2<A, V, S>, kThreads, 0) != hipSuccess ||
+            nb < 1)
+            nb = 1;
+        per_cu = nb;
+    }
+    const uint32_t nbatch = ((uint32_t)p.nblk + 63u) >> 6;
+    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
+    const uint32_t cap = (uint32_t)(num_cus * per_cu);
+    hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, p, t, dev,
+                       coef, var_num, fb);
+    return hipGetLastError();
+}
+
+hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
+                              int16_t *coef, int32_t *var_num, unsigned long long *fallbacks, hipStream_t stream,
+                              int variant, int num_cus) {
+    const bool a = adaptive != 0, v = var_num != nullptr, s = fallbacks != nullptr;
+    if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (p, t, dev, coef, var_num, fallbacks, stream));
+    DCTQ_SELECT(return launch_v2, a, v, s, (p, t, dev, coef, var_num, fallbacks, stream, num_cus));
+}
 }  // namespace dctq

@@ -1,0 +1,120 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/*.h
+declares; host-side tables are bit-identical to the reference's; argument
+validation fails loudly; no compute is attempted without a GPU."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from dct_amd.build import build
+    build()
+    import dct_amd
+    return dct_amd.lib()
+
+
+def declared_functions():
+    names = set()
+    for h in os.listdir(os.path.join(ROOT, "include")):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\(", src, flags=re.M):
+            name = m.group(1)
+            if name not in ("if", "while", "for", "return", "sizeof", "defined"):
+                names.add(name)
+    return names
+
+
+def test_every_declared_symbol_exported(lib):
+    names = declared_functions()
+    # the reference's per-block API (include/dct.h, quantization.h, utils.h) must all be there
+    ref_api = {"dct_init", "dct_free", "dct_forward", "dct_inverse", "create_block_from_pixels",
+               "copy_block_to_coefficients", "quant_init", "quant_free", "generate_quant_matrix",
+               "generate_dequant_matrix", "quantize", "dequantize", "calculate_block_variance",
+               "adjust_matrix_for_block", "alloc_array", "free_array", "alloc_int_array", "free_int_array"}
+    assert ref_api <= names, ref_api - names
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "dct_amd", "libdct_amd.so")],
+                         capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    missing = names - exported
+    assert not missing, missing
+    for n in names:
+        getattr(lib, n)
+
+
+def test_host_tables_match_reference(lib, blocks):
+    import dct_amd
+    for q in [0, 1, 10, 25, 49, 50, 51, 75, 90, 99, 100, 101]:
+        w, thr, d, qm = dct_amd.debug_tables(q)
+        assert (d.view(np.uint64) == np.array(blocks["dct8"], np.uint64)).all()
+        assert (qm.view(np.uint64) == np.array(blocks[f"q8_{q}"], np.uint64)).all(), q
+        assert (thr > 0.49).all() and (thr < 0.5).all()
+        for adaptive in (0, 1):
+            _, thr_a, _, _ = dct_amd.debug_tables(q, adaptive)
+            assert (thr_a <= thr + 1e-12).all() if adaptive else True
+
+
+def test_fastdiv(lib):
+    rng = np.random.default_rng(0)
+    for d in [1, 2, 3, 7, 60, 240, 480, 32400, 129600, 8294400, 2**31 - 1]:
+        for n in list(rng.integers(0, 2**31 - 1, 200)) + [0, d - 1, d, d + 1, 2**31 - 1]:
+            assert lib.dctq_debug_fastdiv(d, int(n)) == int(n) // d, (d, n)
+
+
+def test_error_strings(lib):
+    import dct_amd
+    assert dct_amd.lib().dctq_error_string(0) == b"ok"
+    assert dct_amd.lib().dctq_error_string(-1)
+
+
+def test_c_hosts_compile_and_link(lib):
+    out = subprocess.run(["make", "-C", os.path.join(ROOT, "host")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+
+
+def test_headers_compile_as_c99(tmp_path):
+    src = tmp_path / "t.c"
+    src.write_text('#include "dct.h"\n#include "quantization.h"\n#include "utils.h"\n#include "dct_amd.h"\n'
+                   "int main(void){DCTContext c; QuantContext q; dctq_plane p; (void)c; (void)q; (void)p; return 0;}\n")
+    out = subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic",
+                          "-I" + os.path.join(ROOT, "include"), "-c", str(src), "-o", str(tmp_path / "t.o")],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+
+
+def test_struct_layouts_match_reference():
+    """DCTContext / QuantContext are public in the reference (include/dct.h:21-25,
+    include/quantization.h:18-24): same field order, offsets and size."""
+    code = r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "dct.h"
+#include "quantization.h"
+int main(void){
+ printf("%zu %zu %zu %zu\n", sizeof(DCTContext), offsetof(DCTContext, block_size), offsetof(DCTContext, dct_matrix), offsetof(DCTContext, transposed_dct));
+ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(QuantContext), offsetof(QuantContext, block_size), offsetof(QuantContext, quality), offsetof(QuantContext, quant_matrix), offsetof(QuantContext, dequant_matrix), offsetof(QuantContext, adaptive));
+ return 0;}
+'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        res = {}
+        incs = {"ours": os.path.join(ROOT, "include")}
+        if os.path.isdir("/root/reference/include"):
+            incs["ref"] = "/root/reference/include"
+        for tag, inc in incs.items():
+            p = os.path.join(td, f"{tag}.c")
+            open(p, "w").write(code)
+            exe = os.path.join(td, tag)
+            out = subprocess.run(["gcc", "-std=c99", "-I" + inc, p, "-o", exe], capture_output=True, text=True)
+            assert out.returncode == 0, out.stderr
+            res[tag] = subprocess.run([exe], capture_output=True, text=True).stdout
+        assert res["ours"].split() == ["24", "0", "8", "16", "32", "0", "4", "8", "16", "24"]
+        if "ref" in res:
+            assert res["ours"] == res["ref"]

@@ -1,0 +1,120 @@
+"""CPU: pin the oracle (oracle/dct_oracle.c) to the reference's golden vectors.
+
+The fixtures in tests/golden/ were produced by the reference itself
+(tests/golden/make_golden.py over oracle/_ref/libref.so); these tests show the
+clean-room restatement reproduces them bit for bit, so the GPU tests can use it
+as the checker at sizes the fixtures do not cover."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import f64
+
+QUALITIES = [1, 10, 25, 50, 75, 90, 100]
+
+
+def test_tables_bit_exact(blocks):
+    for n in (4, 8, 16):
+        assert (O.dct_matrix(n).ravel().view(np.uint64) == np.array(blocks[f"dct{n}"], np.uint64)).all()
+        for q in [0, 1, 10, 25, 49, 50, 51, 75, 90, 99, 100, 101]:
+            cq = O.orc().orc_clamp_quality(q)
+            assert cq == blocks[f"clamped_{q}"]
+            qm = O.quant_matrix(n, cq)
+            assert (qm.ravel().view(np.uint64) == np.array(blocks[f"q{n}_{q}"], np.uint64)).all(), (n, q)
+            dq = O.dequant_matrix(qm)
+            assert (dq.ravel().view(np.uint64) == np.array(blocks[f"dq{n}_{q}"], np.uint64)).all(), (n, q)
+
+
+def test_example_block(blocks):
+    from golden.make_golden import EXAMPLE
+    x = EXAMPLE.reshape(8, 8).astype(np.float64) - 128.0
+    c = O.forward(x)
+    assert (c.ravel().view(np.uint64) == np.array(blocks["example_forward"], np.uint64)).all()
+    assert c[0, 0] == -415.37499999999994  # SURVEY 4 known answer
+    var = O.variance(x)
+    assert var == blocks["example_variance"]
+    for q in QUALITIES:
+        for ad in (0, 1):
+            qi = O.quantize(c, q, ad, var)
+            assert qi.ravel().tolist() == blocks[f"example_q{q}_a{ad}"], (q, ad)
+            dq = O.dequantize(qi, q, ad, var)
+            assert (dq.ravel().view(np.uint64) == np.array(blocks[f"example_dq{q}_a{ad}"], np.uint64)).all()
+            rec = O.inverse(dq)
+            assert (rec.ravel().view(np.uint64) == np.array(blocks[f"example_recon{q}_a{ad}"], np.uint64)).all()
+    # textbook JPEG q50 result (tests/test_entropy.c output)
+    assert blocks["example_q50_a0"][:8] == [-26, -3, -6, 2, 2, -1, 0, 0]
+    assert blocks["example_q90_a0"][:8] == [-130, -14, -31, 9, 12, -3, 0, 0]
+    assert (O.inverse(c).ravel().view(np.uint64) == np.array(blocks["example_inverse_of_forward"], np.uint64)).all()
+
+
+def test_example_block_psnr(blocks):
+    """Bug-compatible round trip PSNR of the example block (tests/test_entropy.c:376-393)."""
+    from golden.make_golden import EXAMPLE
+    rec = f64(blocks["example_recon50_a0"]) + 128.0
+    rec = np.clip(rec, 0, 255)
+    mse = np.mean((EXAMPLE.astype(np.float64) - rec) ** 2)
+    assert round(10 * np.log10(255 * 255 / mse), 2) == 13.21
+
+
+def test_adjust(blocks):
+    q = O.quant_matrix(8, 50)
+    dq = O.dequant_matrix(q)
+    for vv in (0.0, 8.02, 99.5, 500.0, 864.2, 1000.0, 5000.0):
+        for isq in (0, 1):
+            m = O.adjust(q if isq else dq, vv, isq)
+            assert (m.ravel().view(np.uint64) == np.array(blocks[f"adjust_50_{vv}_{isq}"], np.uint64)).all()
+
+
+def test_other_block_sizes(blocks):
+    for n in (4, 16):
+        x = np.array(blocks[f"blk{n}_in"], np.float64).reshape(n, n)
+        assert (O.forward(x).ravel().view(np.uint64) == np.array(blocks[f"blk{n}_forward"], np.uint64)).all()
+        assert (O.inverse(x).ravel().view(np.uint64) == np.array(blocks[f"blk{n}_inverse"], np.uint64)).all()
+
+
+@pytest.mark.parametrize("kind", ["uniform", "smooth", "const", "extreme"])
+def test_tiles(tiles, kind):
+    px = tiles[f"{kind}_px"]
+    assert np.array_equal(px, O.synth_plane(12345, O.KINDS[kind], 128, 128))
+    for q in QUALITIES:
+        for ad in (0, 1):
+            assert np.array_equal(O.forward_plane(px, q, ad), tiles[f"{kind}_q{q}_a{ad}"]), (kind, q, ad)
+    _, fl = O.forward_plane(px, 50, 0, want_float=True)
+    assert (fl[:32].view(np.uint64) == tiles[f"{kind}_forward32"].view(np.uint64)).all()
+
+
+def test_full_size_digests(digests):
+    """BASELINE sizes: sha256 of the oracle's int16 planes == the reference's."""
+    for e in digests["entries"]:
+        px = O.synth_plane(digests["seed"], O.KINDS[e["kind"]], e["width"], e["height"])
+        co = O.forward_plane(px, e["quality"], e["adaptive"], 8)
+        assert hashlib.sha256(co.tobytes()).hexdigest() == e["sha256"], e
+
+
+def test_oracle_vs_compiled_reference_random():
+    """Where the compiled reference is present (this container), cross-check random blocks."""
+    if not O.ref_available():
+        pytest.skip("oracle/_ref/libref.so not built here")
+    r = O.ref()
+    rng = np.random.default_rng(99)
+    for _ in range(300):
+        x = rng.integers(-128, 128, (8, 8)).astype(np.float64)
+        a = np.zeros(64)
+        r.ref_forward(8, x.ravel().copy(), a)
+        assert (a.view(np.uint64) == O.forward(x).ravel().view(np.uint64)).all()
+        var = O.variance(x)
+        for q in (int(rng.integers(1, 101)),):
+            for ad in (0, 1):
+                qi = np.zeros(64, np.int32)
+                r.ref_quantize(8, q, ad, var, a, qi)
+                assert (qi == O.quantize(a.reshape(8, 8), q, ad, var).ravel()).all()
+
+
+def test_synth_kinds_are_distinct():
+    a = [O.synth_plane(1, k, 64, 64) for k in range(4)]
+    assert len({x.tobytes() for x in a}) == 4
+    assert set(np.unique(a[3])) <= {0, 255}
+    c = a[2].reshape(8, 8, 8, 8).transpose(0, 2, 1, 3).reshape(64, 64)
+    assert (c == c[:, :1]).all()  # constant 8x8 blocks

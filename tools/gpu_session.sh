@@ -28,6 +28,9 @@ for step in "$@"; do
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu ;;
     pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
     pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmcsq) run pmcsq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    pmcsq2) run pmcsq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU -d $OUT/pmc_sq2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    list) run list 120 rocprofv3 -L ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
