@@ -24,6 +24,8 @@ struct dctq_plan {
     dctq::DevTables host;        // host copy of the device tables
     dctq::DevTables *dev;        // device copy
     unsigned long long *fallbacks;
+    void *ring;                  // v2 tie-path pixel stash (one stream at a time per plan)
+    int ring_wgs;                // workgroups the stash is sized for
 };
 
 namespace {
@@ -79,6 +81,11 @@ void fill_fast_tables(const double *q, int adaptive, FastTables *t) {
         if ((double)t2 > tt) t2 = nextafterf(t2, 0.0f);
         t->thr2[c] = t2;
     }
+    for (int p = 0; p < 64; ++p) {
+        const int c = (((p >> 1) & 7) << 3) + ((p >> 4) << 1) + (p & 1);
+        t->ws[p] = t->w[c];
+        t->t2s[p] = t->thr2[c];
+    }
 }
 }  // namespace dctq
 
@@ -121,6 +128,13 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
         (void)hipFree(p->dev);
         delete p;
         return fail(DCTQ_EHIP, "hipMemcpy(plan tables)", e);
+    }
+    p->ring_wgs = p->num_cus * 4;  // the v2 grid: at most 4 resident 256-thread workgroups per CU (LDS-bound)
+    e = hipMalloc(&p->ring, dctq::fdct8_ring_bytes(p->ring_wgs));
+    if (e != hipSuccess) {
+        (void)hipFree(p->dev);
+        delete p;
+        return fail(DCTQ_ENOMEM, "hipMalloc(tie-path stash)", e);
     }
     *out = p;
     return DCTQ_OK;
@@ -168,6 +182,7 @@ int dctq_plan_from_context(const QuantContext *qctx, dctq_plan **plan) {
 void dctq_plan_destroy(dctq_plan *plan) {
     if (!plan) return;
     (void)hipFree(plan->dev);
+    (void)hipFree(plan->ring);
     delete plan;
 }
 
@@ -184,7 +199,8 @@ int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *co
     int rc = plane_args(src, &a);
     if (rc) return rc;
     HIPCHK(dctq::launch_fdct8_quant(a, plan->fast, plan->dev, plan->adaptive, coef, var_num, plan->fallbacks,
-                                    (hipStream_t)stream, plan->variant, plan->num_cus),
+                                    (hipStream_t)stream, plan->variant, plan->num_cus, plan->ring,
+                                    plan->ring_wgs),
            "fdct8_quant launch");
     return DCTQ_OK;
 }

@@ -18,6 +18,8 @@ struct FastTables {
     float w[64];    // S_i S_j / Q_ij  (AAN output scale folded into 1/Q)
     float thr[64];  // |frac| above which the exact fp64 path decides (guard band)
     float thr2[64]; // thr^2 rounded down: flag iff thr2 - f*f < 0
+    // v2 processing order: slot p = 16*cp + 2*i + h holds coefficient 8*i + 2*cp + h
+    float ws[64], t2s[64];
 };
 
 // Per-plan device-resident tables (runtime-indexed: exact tie path, inverse).
@@ -42,7 +44,9 @@ struct PlaneArgs {
 
 hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
                               int16_t *coef, int32_t *var_num, unsigned long long *fallbacks,
-                              hipStream_t stream, int variant, int num_cus);
+                              hipStream_t stream, int variant, int num_cus, void *ring, int ring_wgs);
+// bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
+size_t fdct8_ring_bytes(int workgroups);
 hipError_t launch_fdct8_float(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);
 hipError_t launch_idct8(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
                         long long nblk, float *recon, hipStream_t stream);

@@ -252,18 +252,27 @@ __global__ __launch_bounds__(kThreads) void fdct8_quant_v1(PlaneArgs p, FastTabl
 // v2 (default): persistent grid-stride kernel, sized for the gfx950 VALU cost
 // model measured in profiles/r01/valu_issue_rates.md.
 //  * each wave walks 64-block batches b, b+W, b+2W, ... and prefetches the next
-//    batch's 8 rows into registers while it computes the current one;
+//    batch's 8 rows (non-temporal) while it computes the current one;
 //  * u8 -> fp32 with v_cvt_f32_ubyteN (inline asm, so the compiler cannot turn
 //    the first butterfly stage into half-rate SDWA integer adds + converts);
-//  * quantization in packed fp32 (the per-plan tables sit in SGPR pairs, which
-//    v_pk_* ops read at no extra cost), tie flags as sign bits of thr^2 - f^2
-//    shifted into a per-lane 64-bit mask with v_alignbit;
+//  * the second butterfly pass runs two columns at a time, fused with the
+//    quantization of those 16 coefficients, whose packed int16 pairs go straight
+//    to the LDS stage (16 of the 64 second-pass values live at a time);
+//  * quantization in packed fp32 (the per-plan tables are read through scalar
+//    loads in processing order), tie flags as sign bits of thr^2 - f^2 shifted
+//    into a per-lane 64-bit mask with v_alignbit;
+//  * the LDS stage is written out as 1 KiB-contiguous buffer stores (num_records
+//    clips the tail, so the stores are unconditional);
 //  * flagged (block, coefficient) pairs go to a wave-local LDS queue and are
-//    recomputed exactly 64 at a time (every lane busy), then patched in HBM --
-//    instead of stalling the whole wave on one lane's fp64 work.
+//    recomputed exactly 64 at a time (every lane busy), then patched in HBM.
 typedef float f2 __attribute__((ext_vector_type(2)));
-constexpr int kQCap = 128;
-constexpr int kPitch2 = 136;  // bytes per block in the v2 stage: 2-way (free) conflicts for the b32 writes  // per-wave tie queue; holds < 64 between rounds + one round of <= 64
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+constexpr int kQCap = 128;     // per-wave tie queue: < 64 between rounds + one round of <= 64
+constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) conflicts for the b32 writes
+#ifndef DCTQ_ABLATE
+#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run
+#endif
 
 template <int K>
 __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
@@ -275,204 +284,298 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
     return f;
 }
 
+// Pixel rows are read exactly once: non-temporal loads (+8.7 % on the memory
+// ceiling of this stream, profiles/r01/valu_issue_rates.md).
 __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 (&rows)[8]) {
     const uint8_t *px = block_ptr(p, n < (uint32_t)p.nblk ? n : 0);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) rows[r] = *reinterpret_cast<const uint2 *>(px + r * p.stride);
+    for (int r = 0; r < 8; ++r) {
+        const u2v t = __builtin_nontemporal_load(reinterpret_cast<const u2v *>(px + r * p.stride));
+        rows[r] = make_uint2(t.x, t.y);
+    }
 }
 
 // Exact reference-order quantization of coefficient c of the block at px (one
-// queue entry): exact_quant() above plus, for adaptive plans, the block's exact
-// variance and adjusted divisor (src/quantization.c:153-211).
+// queue entry): the arithmetic of exact_quant() above plus, for adaptive plans,
+// the block's exact variance and adjusted divisor (src/quantization.c:153-211).
+// A drain runs 64 of these at once (one per lane), so latency matters: all 8
+// pixel rows and the 16 table entries are requested before the fp64 chain.
 template <bool ADAPTIVE>
-__device__ int exact_entry(const uint8_t *__restrict__ px, long long stride, int c, const DevTables *__restrict__ dev) {
+__device__ int exact_entry(const uint4 *__restrict__ stash, int c, const DevTables *__restrict__ dev) {
+    const int i = c >> 3, j = c & 7;
+    uint2 rows[8];
+    double dj[8], di[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint4 w = stash[k];  // rows 2k, 2k+1 of the block, stashed when the entry was queued
+        rows[2 * k] = make_uint2(w.x, w.y);
+        rows[2 * k + 1] = make_uint2(w.z, w.w);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        dj[k] = dev->dct[j * 8 + k];  // D^T[k][j]
+        di[k] = dev->dct[i * 8 + k];  // D[i][k]
+    }
     double m = dev->quant[c];
     if (ADAPTIVE && c != 0) {
         uint32_t s1 = 0, s2 = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint2 row = *reinterpret_cast<const uint2 *>(px + k * stride);
-            s1 = __builtin_amdgcn_udot4(row.x, 0x01010101u, s1, false);
-            s1 = __builtin_amdgcn_udot4(row.y, 0x01010101u, s1, false);
-            s2 = __builtin_amdgcn_udot4(row.x, row.x, s2, false);
-            s2 = __builtin_amdgcn_udot4(row.y, row.y, s2, false);
+            s1 = __builtin_amdgcn_udot4(rows[k].x, 0x01010101u, s1, false);
+            s1 = __builtin_amdgcn_udot4(rows[k].y, 0x01010101u, s1, false);
+            s2 = __builtin_amdgcn_udot4(rows[k].x, rows[k].x, s2, false);
+            s2 = __builtin_amdgcn_udot4(rows[k].y, rows[k].y, s2, false);
         }
         const int32_t sx = (int32_t)s1 - 8192;
         const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
         m = m * adaptive_scale(64 * sxx - sx * sx);
         if (m < 1.0) m = 1.0;
     }
-    return exact_quant(px, stride, c, dev->dct, m);
+    // temp[k][j] = sum_l x[k][l] D^T[l][j]; out = sum_k D[i][k] temp[k][j]  (src/dct.c:57-74)
+    double out = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const uint32_t w = l < 4 ? rows[k].x : rows[k].y;
+            t += ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
+        }
+        out += di[k] * t;
+    }
+    return (int)round(out / m);
 }
 
 template <bool ADAPTIVE, bool STATS>
-__device__ __forceinline__ void drain_queue(const PlaneArgs &p, const DevTables *__restrict__ dev,
-                                            int16_t *__restrict__ coef, const uint32_t *q, int &qn, int lane,
+__device__ __forceinline__ void drain_queue(const DevTables *__restrict__ dev, int16_t *__restrict__ coef,
+                                            const uint32_t *q, const uint4 *ring, int &qn, int lane,
                                             unsigned long long *fallbacks) {
-    // the wave's own coefficient stores must land before their patches
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the wave's own coefficient stores (and its stash stores) must land first
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     const int take = qn < 64 ? qn : 64;
     if (lane < take) {
-        const uint32_t e = q[qn - take + lane];
+        const int slot = qn - take + lane;
+        const uint32_t e = q[slot];
         const uint32_t n = e >> 6;
         const int c = (int)(e & 63u);
-        const int val = exact_entry<ADAPTIVE>(block_ptr(p, n), p.stride, c, dev);
+        const int val = exact_entry<ADAPTIVE>(ring + slot * 4, c, dev);
         coef[(size_t)n * 64 + c] = (int16_t)val;
     }
     qn -= take;
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // nothing of this rare path stays in flight
 }
 
+// One 64-block batch of the v2 loop.  `nxt` holds this batch's rows on entry and
+// the next batch's rows on exit.
 template <bool ADAPTIVE, bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneArgs p, FastTables t,
-                                                           const DevTables *__restrict__ dev,
-                                                           int16_t *__restrict__ coef,
-                                                           int32_t *__restrict__ var_out,
-                                                           unsigned long long *fallbacks) {
-    __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ uint32_t queue[kWaves * kQCap];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t nbatch = ((uint32_t)p.nblk + 63u) >> 6;
-    const uint32_t step = gridDim.x * kWaves;
-    uint32_t *q = queue + wv * kQCap;
-    int qn = 0;
+__device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables *__restrict__ dev,
+                                            int16_t *__restrict__ coef, int32_t *__restrict__ var_out,
+                                            unsigned long long *fallbacks, uint4 *stage, uint32_t *q, uint4 *ring,
+                                            int &qn, uint2 (&nxt)[8], uint32_t b, uint32_t step, int lane, int wv) {
     const f2 M2 = {kMagic, kMagic};
-
-    uint32_t b = blockIdx.x * kWaves + wv;
-    uint2 nxt[8];
-    if (b < nbatch) load_rows(p, b * 64 + lane, nxt);
-    for (; b < nbatch; b += step) {
-        uint2 cur[8];
+    uint2 cur[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-        const uint32_t n = b * 64 + lane;
-        const bool valid = n < (uint32_t)p.nblk;
-        if (b + step < nbatch) load_rows(p, (b + step) * 64 + lane, nxt);
+    for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+    const uint32_t n = b * 64 + lane;
+    const bool valid = n < (uint32_t)p.nblk;
+    load_rows(p, (b + step) * 64 + lane, nxt);  // unconditional: past the end it re-reads block 0
 
-        float v[8][8];
+    float v[8][8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        v[r][0] = cvt_ubyte<0>(cur[r].x);
+        v[r][1] = cvt_ubyte<1>(cur[r].x);
+        v[r][2] = cvt_ubyte<2>(cur[r].x);
+        v[r][3] = cvt_ubyte<3>(cur[r].x);
+        v[r][4] = cvt_ubyte<0>(cur[r].y);
+        v[r][5] = cvt_ubyte<1>(cur[r].y);
+        v[r][6] = cvt_ubyte<2>(cur[r].y);
+        v[r][7] = cvt_ubyte<3>(cur[r].y);
+    }
+    int32_t var_num = 0;
+    if (ADAPTIVE || VAR) {
+        uint32_t s1 = 0, s2 = 0;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            v[r][0] = cvt_ubyte<0>(cur[r].x);
-            v[r][1] = cvt_ubyte<1>(cur[r].x);
-            v[r][2] = cvt_ubyte<2>(cur[r].x);
-            v[r][3] = cvt_ubyte<3>(cur[r].x);
-            v[r][4] = cvt_ubyte<0>(cur[r].y);
-            v[r][5] = cvt_ubyte<1>(cur[r].y);
-            v[r][6] = cvt_ubyte<2>(cur[r].y);
-            v[r][7] = cvt_ubyte<3>(cur[r].y);
+            s1 = __builtin_amdgcn_udot4(cur[r].x, 0x01010101u, s1, false);
+            s1 = __builtin_amdgcn_udot4(cur[r].y, 0x01010101u, s1, false);
+            s2 = __builtin_amdgcn_udot4(cur[r].x, cur[r].x, s2, false);
+            s2 = __builtin_amdgcn_udot4(cur[r].y, cur[r].y, s2, false);
         }
-        int32_t var_num = 0;
-        if (ADAPTIVE || VAR) {
-            uint32_t s1 = 0, s2 = 0;
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                s1 = __builtin_amdgcn_udot4(cur[r].x, 0x01010101u, s1, false);
-                s1 = __builtin_amdgcn_udot4(cur[r].y, 0x01010101u, s1, false);
-                s2 = __builtin_amdgcn_udot4(cur[r].x, cur[r].x, s2, false);
-                s2 = __builtin_amdgcn_udot4(cur[r].y, cur[r].y, s2, false);
-            }
-            const int32_t sx = (int32_t)s1 - 8192;
-            const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
-            var_num = 64 * sxx - sx * sx;
-            if (VAR && valid) var_out[n] = var_num;
-        }
+        const int32_t sx = (int32_t)s1 - 8192;
+        const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
+        var_num = 64 * sxx - sx * sx;
+    }
 
-        // ---- row pass, then column pairs fused with quantization: Y(i, c0..c0+1) is
-        // quantized right after its two columns are transformed and the packed int16
-        // pair goes straight to the LDS stage, so only 16 of the 64 values of the
-        // second pass are ever live (the block itself stays in registers).
+    // ---- row pass, then column pairs fused with quantization
 #pragma unroll
-        for (int r = 0; r < 8; ++r)
+    for (int r = 0; r < 8; ++r)
+        if (!(DCTQ_ABLATE & 2))
             aan8(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7], DCTQ_C4, DCTQ_C6,
                  DCTQ_C2MC6, DCTQ_C2PC6);
 
-        f2 sc2 = {1.0f, 1.0f};
-        if (ADAPTIVE) {
-            const float inv = (float)(1.0 / adaptive_scale(var_num));
-            sc2 = f2{inv, inv};
-        }
-        // Per-plan tables through an opaque per-iteration pointer: scalar loads
-        // stay inside the loop instead of being hoisted into 128 live SGPRs.
-        const FastTables *tp = &dev->fast;
-        asm volatile("" : "+s"(tp));
-        uint32_t mlo = 0, mhi = 0;  // bit (31 - p%32): processing slot p = 16*cp + 2*i + h flagged
-        uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
+    f2 sc2 = {1.0f, 1.0f};
+    if (ADAPTIVE) {
+        const float inv = (float)(1.0 / adaptive_scale(var_num));
+        sc2 = f2{inv, inv};
+    }
+    // Per-plan tables through an opaque per-batch pointer in the constant address
+    // space: scalar loads stay inside the loop (hoisted, they would need 128 live
+    // SGPRs) and stay scalar (a generic pointer becomes flat_load + vmcnt(0)).
+    const FastTables *tg = &dev->fast;
+    asm volatile("" : "+s"(tg));
+    const __attribute__((address_space(4))) FastTables *tp = (const __attribute__((address_space(4))) FastTables *)tg;
+    uint32_t mlo = 0, mhi = 0;  // bit (31 - p%32): processing slot p = 16*cp + 2*i + h flagged
+    uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
 #pragma unroll
-        for (int cp = 0; cp < 4; ++cp) {
-            const int c0 = 2 * cp;
+    for (int cp = 0; cp < 4; ++cp) {
+        const int c0 = 2 * cp;
+        if (!(DCTQ_ABLATE & 2)) {
             aan8(v[0][c0], v[1][c0], v[2][c0], v[3][c0], v[4][c0], v[5][c0], v[6][c0], v[7][c0], DCTQ_C4, DCTQ_C6,
                  DCTQ_C2MC6, DCTQ_C2PC6);
             aan8(v[0][c0 + 1], v[1][c0 + 1], v[2][c0 + 1], v[3][c0 + 1], v[4][c0 + 1], v[5][c0 + 1], v[6][c0 + 1],
                  v[7][c0 + 1], DCTQ_C4, DCTQ_C6, DCTQ_C2MC6, DCTQ_C2PC6);
-            if (cp == 0) v[0][0] -= 8192.0f;  // 64 * 128: exact (integer < 2^24)
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int c = i * 8 + c0;
-                const f2 y = {v[i][c0], v[i][c0 + 1]};
-                f2 w = {tp->w[c], tp->w[c + 1]};
-                if (ADAPTIVE) {
-                    if (c == 0) w.y *= sc2.y;  // the DC keeps Q (src/quantization.c:198-199)
-                    else w *= sc2;
-                }
-                const f2 tt = __builtin_elementwise_fma(y, w, M2);
-                const f2 nr = M2 - tt;
-                const f2 f = __builtin_elementwise_fma(y, w, nr);
-                const f2 T = {tp->thr2[c], tp->thr2[c + 1]};
-                const f2 d = __builtin_elementwise_fma(-f, f, T);  // < 0  <=>  |f| beyond the guard
-                if (cp < 2) {
-                    mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.x), 31);
-                    mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.y), 31);
-                } else {
-                    mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.x), 31);
-                    mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.y), 31);
-                }
-                st32[i * 4 + cp] = __builtin_amdgcn_perm(__float_as_uint(tt.y), __float_as_uint(tt.x), 0x05040100u);
-            }
-            // Pin the flag mask here: otherwise LLVM sinks the 32 residual tests of
-            // this column pair to their only use (the queue phase, after the
-            // stores) and keeps every residual live across the stores.
-            asm volatile("" : "+v"(mlo), "+v"(mhi));
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint4 *dst = reinterpret_cast<uint4 *>(coef) + (size_t)b * 64 * 8;
+        if (cp == 0) v[0][0] -= 8192.0f;  // 64 * 128: exact (integer < 2^24)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int c = i * 8 + c0, slot = 16 * cp + 2 * i;
+            const f2 y = {v[i][c0], v[i][c0 + 1]};
+            f2 w = {tp->ws[slot], tp->ws[slot + 1]};
+            if (ADAPTIVE) {
+                if (c == 0) w.y *= sc2.y;  // the DC keeps Q (src/quantization.c:198-199)
+                else w *= sc2;
+            }
+            const f2 tt = __builtin_elementwise_fma(y, w, M2);
+            const f2 nr = M2 - tt;
+            const f2 f = __builtin_elementwise_fma(y, w, nr);
+            const f2 T = {tp->t2s[slot], tp->t2s[slot + 1]};
+            const f2 d = __builtin_elementwise_fma(-f, f, T);  // < 0  <=>  |f| beyond the guard
+            if (DCTQ_ABLATE & 1) {
+            } else if (cp < 2) {
+                mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.x), 31);
+                mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.y), 31);
+            } else {
+                mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.x), 31);
+                mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.y), 31);
+            }
+            st32[i * 4 + cp] = __builtin_amdgcn_perm(__float_as_uint(tt.y), __float_as_uint(tt.x), 0x05040100u);
+        }
+        // Pin the flag mask here: otherwise LLVM sinks the 32 residual tests of
+        // this column pair to their only use (the queue phase, after the stores)
+        // and keeps every residual live across the stores.
+        asm volatile("" : "+v"(mlo), "+v"(mhi));
+    }
+
+    // Consume the prefetched rows HERE, before this batch's stores are issued:
+    // the wait the compiler puts in front of this fence then covers loads issued
+    // a whole compute phase ago and nothing younger.  Left to itself it waits at
+    // the top of the next batch, where LLVM orders the youngest load against
+    // younger loads only and emits vmcnt(0) -- which on gfx950 (one in-order
+    // counter for loads and stores) also drains this batch's stores.
+    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    {
+        // Stores through a buffer descriptor whose num_records ends at the last
+        // valid block: out-of-range lanes are dropped by the hardware, so the
+        // stores are unconditional (predicated stores made the waitcnt pass give
+        // up and wait vmcnt(0) at the loop latch).
+        const uint32_t left = (uint32_t)p.nblk - b * 64;
+        const uint32_t nb = left < 64u ? left : 64u;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<char *>(coef) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
         const uint2 *st64 = reinterpret_cast<const uint2 *>(stage) + wv * 64 * (kPitch2 / 8);
+        // all 8 chunks into distinct registers first, one voffset register and
+        // per-store soffsets: a store's VGPR operands must not be overwritten
+        // while it is in flight (reuse would put vmcnt waits between the stores)
+        u4v val[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int m = k * 64 + lane;
             const int bl = m >> 3;
             const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
-            if (b * 64 + bl < (uint32_t)p.nblk) dst[m] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            val[k] = u4v{lo.x, lo.y, hi.x, hi.y};
         }
-
-        // ---- defer flagged coefficients to the wave's queue (rare: ~1.5 per batch at q50)
-        if (!valid) mlo = mhi = 0;
-        uint64_t has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
-        while (has) {
-            if (qn > kQCap - 64) drain_queue<ADAPTIVE, STATS>(p, dev, coef, q, qn, lane, fallbacks);
-            if (mlo | mhi) {
-                int slot;
-                if (mlo) {
-                    slot = __clz(mlo);
-                    mlo &= ~(0x80000000u >> slot);
-                } else {
-                    const int k = __clz(mhi);
-                    mhi &= ~(0x80000000u >> k);
-                    slot = 32 + k;
-                }
-                // slot = 16*cp + 2*i + h  ->  coefficient 8*i + 2*cp + h
-                const int c = (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
-                const uint32_t pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
-                q[pos] = (n << 6) | (uint32_t)c;
-            }
-            qn += __builtin_popcountll(has);
-            has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, 0);
+        if (VAR) {
+            const __amdgpu_buffer_rsrc_t rv =
+                __builtin_amdgcn_make_buffer_rsrc(var_out + (size_t)b * 64, (short)0, (int)(nb * 4u), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, 0);
         }
-        if (qn >= 64) drain_queue<ADAPTIVE, STATS>(p, dev, coef, q, qn, lane, fallbacks);
     }
-    while (qn > 0) drain_queue<ADAPTIVE, STATS>(p, dev, coef, q, qn, lane, fallbacks);
+
+    // ---- defer flagged coefficients to the wave's queue (rare: ~1.5 per batch at q50)
+    if (!valid || (DCTQ_ABLATE & 8)) mlo = mhi = 0;
+    if (DCTQ_ABLATE & 32) asm volatile("" : "+v"(mlo), "+v"(mhi), "+s"(qn));  // keep code, never run (diagnostic)
+    uint64_t has = __builtin_amdgcn_ballot_w64((DCTQ_ABLATE & 32) ? (mlo == 0x12345u && mhi == 0x6789u) : (mlo | mhi) != 0);
+    while (has) {
+        if (qn > kQCap - 64) {
+            if (DCTQ_ABLATE & 16) qn = 0;
+            else drain_queue<ADAPTIVE, STATS>(dev, coef, q, ring, qn, lane, fallbacks);
+        }
+        if (mlo | mhi) {
+            int slot;
+            if (mlo) {
+                slot = __clz(mlo);
+                mlo &= ~(0x80000000u >> slot);
+            } else {
+                const int k = __clz(mhi);
+                mhi &= ~(0x80000000u >> k);
+                slot = 32 + k;
+            }
+            // slot = 16*cp + 2*i + h  ->  coefficient 8*i + 2*cp + h
+            const int c = (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
+            const uint32_t pos =
+                qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
+            q[pos] = (n << 6) | (uint32_t)c;
+            // stash the block's pixels while they are still in registers: the
+            // drain must not go back to HBM for them (8 random 64-B bursts per entry)
+            uint4 *st = ring + pos * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) st[k] = make_uint4(cur[2 * k].x, cur[2 * k].y, cur[2 * k + 1].x, cur[2 * k + 1].y);
+        }
+        qn += __builtin_popcountll(has);
+        has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
+    }
+    if (qn >= 64) {
+        if (DCTQ_ABLATE & 16) qn = 0;
+        else drain_queue<ADAPTIVE, STATS>(dev, coef, q, ring, qn, lane, fallbacks);
+    }
+}
+
+template <bool ADAPTIVE, bool VAR, bool STATS>
+__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneArgs p, FastTables t,
+                                                              const DevTables *__restrict__ dev,
+                                                              int16_t *__restrict__ coef,
+                                                              int32_t *__restrict__ var_out,
+                                                              unsigned long long *fallbacks, uint4 *ring_all) {
+    __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ uint32_t queue[kWaves * kQCap];
+    // readfirstlane: the wave index is uniform, so batch pointers and buffer
+    // descriptors live in SGPRs (no waterfall loops around the stores)
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nbatch = ((uint32_t)p.nblk + 63u) >> 6;
+    const uint32_t step = gridDim.x * kWaves;
+    uint32_t *q = queue + wv * kQCap;
+    uint4 *ring = ring_all + (size_t)(blockIdx.x * kWaves + wv) * kQCap * 4;  // 64 B per queue slot
+    int qn = 0;
+    uint32_t b = blockIdx.x * kWaves + wv;
+    uint2 nxt[8];
+    load_rows(p, b * 64 + lane, nxt);
+    // same fence as at the end of a batch: the loop header then sees no load in
+    // flight on either incoming edge and needs no wait at all
+    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    for (; b < nbatch; b += step)
+        fdct8_batch<ADAPTIVE, VAR, STATS>(p, dev, coef, var_out, fallbacks, stage, q, ring, qn, nxt, b, step, lane, wv);
+    if (DCTQ_ABLATE & 16) qn = 0;
+    while (qn > 0) drain_queue<ADAPTIVE, STATS>(dev, coef, q, ring, qn, lane, fallbacks);
 }
 
 #define DCTQ_SELECT(KERN, A, V, S, ...)                                          \
@@ -496,7 +599,8 @@ static hipError_t launch_v1(const PlaneArgs &p, const FastTables &t, const DevTa
 
 template <bool A, bool V, bool S>
 static hipError_t launch_v2(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int16_t *coef,
-                            int32_t *var_num, unsigned long long *fb, hipStream_t stream, int num_cus) {
+                            int32_t *var_num, unsigned long long *fb, hipStream_t stream, int num_cus, void *ring,
+                            int ring_wgs) {
     static int per_cu = 0;  // resident workgroups per CU for this instantiation
     if (per_cu == 0) {
         int nb = 0;
@@ -507,17 +611,20 @@ static hipError_t launch_v2(const PlaneArgs &p, const FastTables &t, const DevTa
     }
     const uint32_t nbatch = ((uint32_t)p.nblk + 63u) >> 6;
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu);
+    uint32_t cap = (uint32_t)(num_cus * per_cu);
+    if (cap > (uint32_t)ring_wgs) cap = (uint32_t)ring_wgs;
     hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, p, t, dev,
-                       coef, var_num, fb);
+                       coef, var_num, fb, (uint4 *)ring);
     return hipGetLastError();
 }
 
+size_t fdct8_ring_bytes(int workgroups) { return (size_t)workgroups * kWaves * kQCap * 64; }
+
 hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
                               int16_t *coef, int32_t *var_num, unsigned long long *fallbacks, hipStream_t stream,
-                              int variant, int num_cus) {
+                              int variant, int num_cus, void *ring, int ring_wgs) {
     const bool a = adaptive != 0, v = var_num != nullptr, s = fallbacks != nullptr;
     if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (p, t, dev, coef, var_num, fallbacks, stream));
-    DCTQ_SELECT(return launch_v2, a, v, s, (p, t, dev, coef, var_num, fallbacks, stream, num_cus));
+    DCTQ_SELECT(return launch_v2, a, v, s, (p, t, dev, coef, var_num, fallbacks, stream, num_cus, ring, ring_wgs));
 }
 }  // namespace dctq

@@ -1,0 +1,46 @@
+"""Time the v2 forward kernel against diagnostic builds with parts removed
+(tools/ubench/ablate.sh), interleaved in one process.  Outputs of the ablated
+builds are wrong by construction; only their time matters."""
+import ctypes as C
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import dct_amd  # noqa: E402
+
+libs = {"full": dct_amd.LIB_PATH}
+for m, name in [(8, "flags-no-queue"), (16, "append-no-drain"), (32, "queue-code-idle")]:
+    p = os.path.join(ROOT, "tools", "ubench", f"libablate_{m}.so")
+    if os.path.exists(p):
+        libs[name] = p
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+px = dct_amd.synth(7, "uniform", 3840, 2160, F)
+d = dct_amd.plane_desc(px)
+nblk = F * 480 * 270
+out = torch.empty((nblk, 64), dtype=torch.int16, device="cuda")
+plans = {}
+for name, path in libs.items():
+    L = C.CDLL(path)
+    L.dctq_plan_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.dctq_forward_quant.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_void_p, C.c_void_p, C.c_void_p]
+    h = C.c_void_p()
+    assert L.dctq_plan_create(50, 0, C.byref(h)) == 0
+    plans[name] = (L, h)
+stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+times = {k: [] for k in plans}
+for r in range(12):
+    for name, (L, h) in plans.items():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        assert L.dctq_forward_quant(h, C.byref(d), C.c_void_p(out.data_ptr()), None, stream) == 0
+        e1.record()
+        torch.cuda.synchronize()
+        if r >= 2:
+            times[name].append(e0.elapsed_time(e1) * 1e-3)
+for name, ts in times.items():
+    med = statistics.median(ts)
+    print(f"{name:24s} median {med*1e6:7.1f} us  {nblk*192/med/1e9:6.0f} GB/s")

@@ -31,6 +31,13 @@ for step in "$@"; do
     pmcsq) run pmcsq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
     pmcsq2) run pmcsq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU -d $OUT/pmc_sq2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
     list) run list 120 rocprofv3 -L ;;
+    ablate) run ablate 300 python tools/ablate_bench.py ;;
+    pmcv2c) run pmcv2c 600 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAIT_INST_ANY SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD -d $OUT/pmc_v2c -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
+    pmcv2d) run pmcv2d 600 rocprofv3 --pmc TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum -d $OUT/pmc_v2d -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
+    pmcv2) run pmcv2 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_v2 -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
+    pmcv2b) run pmcv2b 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA -d $OUT/pmc_v2b -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
+    ab) run ab 300 python tools/ab_bench.py --variants 1,2 ;;
+    abk) run abk 300 bash -c "python tools/ab_bench.py --kind smooth && python tools/ab_bench.py --kind const && python tools/ab_bench.py --adaptive 1 && python tools/ab_bench.py --quality 90" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
