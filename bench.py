@@ -11,7 +11,10 @@ in HBM; one step = dctq_forward_quant over every block of the batch (two
 launches: the F luma planes, then the 2F chroma planes), int16 coefficients
 bit-exact with the reference.  N>1: one process per GPU (torch.distributed),
 each rank its own F frames (weak scaling, no data-path collective); value =
-all blocks / max-over-ranks wall time.
+all blocks / max-over-ranks wall time.  At N>1 a second, separately reported
+leg ("gather") times forward DCT+quant of the luma frames followed by the RCCL
+all-gather of every rank's int16 coefficient planes (BASELINE configs[3],
+SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange.
 
 Also reported: the dominant kernel's roofline (algorithmic 192 B/block over the
 HIP-event-timed launch durations) and the reference's own CPU path
@@ -51,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (wall s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
     return ap.parse_args()
 
 
@@ -82,6 +86,36 @@ def cpu_baseline(args):
                       f"adaptive={args.adaptive}) through ref_forward_plane: create_block_from_pixels -> "
                       f"dct_forward -> calculate_block_variance -> quantize per block, {threads} pthreads "
                       f"over block rows, {el:.1f} s"}
+
+
+def gather_leg(args, plan, luma, coef_y, world, rank, dev):
+    """Forward DCT+quant of this rank's luma frames + RCCL all-gather of all
+    ranks' coefficient planes onto every rank; max-over-ranks wall time."""
+    from dct_amd import shard
+    n = coef_y.shape[0]
+    counts = [n] * world
+
+    def once():
+        plan.forward_quant(luma, out=coef_y)
+        return shard.gather_coefficients(coef_y, counts)
+
+    full = once()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.gather_steps):
+        full = once()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    ok = bool(torch.equal(full[rank * n:(rank + 1) * n], coef_y))
+    return {"op": "forward_quant(luma) + all_gather_into_tensor (RCCL) of int16 coefficient planes",
+            "blocks_per_s": world * n * args.gather_steps / el, "ms_per_step": el / args.gather_steps * 1e3,
+            "bytes_received_per_rank": (world - 1) * n * 128, "steps": args.gather_steps,
+            "own_slice_intact": ok}
 
 
 def main():
@@ -157,6 +191,10 @@ def main():
         except Exception as e:  # noqa: BLE001 -- report, do not hide
             parity = f"error: {e}"
 
+    gather = None
+    if world > 1 and args.gather_steps > 0:
+        gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
+
     total_blocks = world * (nblk_y + nblk_c) * args.steps
     value = total_blocks / el
     traffic = None
@@ -180,7 +218,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8->int16 (fp32 butterfly + exact fp64 tie path)",
+            "dtype": "fp32",
             "data": "synthetic (device splitmix64 frames, kind=%s)" % args.kind,
             "config": {"workload": f"4K 4:2:0 frame stream (BASELINE configs[2] planes), {F} frames/GPU/step, "
                                    f"forward DCT+quant q{args.quality} adaptive={args.adaptive}, int16 out",
@@ -188,10 +226,14 @@ def main():
                        "adaptive": args.adaptive, "parallelism": f"frames sharded over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "fdct8_quant_kernel", "avg_launch_us": avg_launch_s * 1e6,
+                         "kernel": f"fdct8_quant_v2<{bool(args.adaptive)}, false, false>".lower(),
+                         "avg_launch_us": avg_launch_s * 1e6,
                          "bytes_per_launch": avg_launch_bytes},
             "cpu_baseline": cpu,
             "parity_check": parity,
+            "gather": gather,
+            "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
+                    "reference-order recomputation for guard-band (tie) coefficients",
         }
         print(json.dumps(out))
     if world > 1:

@@ -1,0 +1,77 @@
+"""Multi-GPU sharding of the DCT+quant path.
+
+Blocks are independent (quantize reads only the plan and its own block,
+src/quantization.c:113-131), so the path partitions with no data exchange:
+
+* a batch of frames splits into contiguous frame ranges, one per rank;
+* a single large plane splits into contiguous bands of block rows -- a band is
+  itself a plane (pixel pointer advanced by 8*row0*stride, height 8*rows), and
+  its coefficients are a contiguous slice of the raster-order output.
+
+The only collective is the OPTIONAL gather of the int16 coefficient planes
+(BASELINE configs[3]: "RCCL allgather of quantized coefficient planes over
+xGMI"): one all_gather per call over the whole shard, padded to the largest
+shard so ragged splits work.  The ordering of the gathered result equals the
+unsharded raster order, so rank r's slice lands at blocks_before(r).
+"""
+from __future__ import annotations
+
+
+def split(n: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous [lo, hi) share of n units for `rank`; the first n % world ranks get one more."""
+    if world < 1 or not 0 <= rank < world or n < 0:
+        raise ValueError("bad split arguments")
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def frame_shard(px, world: int, rank: int):
+    """Frames [lo, hi) of a [F, H, W] stack owned by `rank` (a view, no copy)."""
+    lo, hi = split(px.shape[0], world, rank)
+    return px[lo:hi], (lo, hi)
+
+
+def band_shard(px, world: int, rank: int):
+    """Block-row band of one [H, W] plane owned by `rank` (a view, no copy).
+    Returns (band, (row0, rows)) in block rows; the band's coefficients are
+    coef[row0 * W/8 : (row0 + rows) * W/8] of the whole plane."""
+    if px.shape[-2] % 8 or px.shape[-1] % 8:
+        raise ValueError("plane dimensions must be multiples of 8")
+    lo, hi = split(px.shape[-2] // 8, world, rank)
+    return px[..., 8 * lo:8 * hi, :], (lo, hi - lo)
+
+
+def gather_coefficients(local, counts, group=None):
+    """All-gather int16 coefficient shards [n_r, 64] (n_r = counts[r]) into the
+    full [sum(counts), 64] tensor on every rank, in rank order.
+
+    One collective over the whole shard (bigger messages, fewer calls: xGMI
+    rings are per-link bound).  Ragged shards are padded to
+    max(counts) and compacted after the exchange."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(counts) != world or local.shape[0] != counts[rank]:
+        raise ValueError("counts must list every rank's shard size")
+    m = max(counts)
+    if local.shape[0] < m:
+        pad = torch.zeros((m - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        send = torch.cat([local, pad])
+    else:
+        send = local.contiguous()
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, send, group=group)
+        if all(c == m for c in counts):
+            return out
+        parts = list(out.split(m))
+    else:  # gloo (CPU tests): no int16 reductions there, so move the raw bytes
+        raw = send.view(torch.uint8)
+        parts = [torch.empty_like(raw) for _ in range(world)]
+        dist.all_gather(parts, raw, group=group)
+        parts = [p.view(local.dtype) for p in parts]
+    if all(c == m for c in counts):
+        return torch.cat(parts)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)])

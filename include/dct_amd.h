@@ -35,7 +35,9 @@ extern "C" {
 
 /* Opaque per-configuration state: the host-computed tables (D of src/dct.c:17-30,
  * Q of src/quantization.c:51-99, fast-path scale and guard tables) uploaded to
- * the device that was current at creation. */
+ * the device that was current at creation, plus a small device workspace for
+ * the exact tie path.  Calls on one plan must be ordered (one stream at a time,
+ * or streams synchronised by the caller); use one plan per concurrent stream. */
 typedef struct dctq_plan dctq_plan;
 
 /* quality is clamped to 1..100 exactly as quant_init does (src/quantization.c:26-31). */

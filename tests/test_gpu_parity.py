@@ -354,3 +354,23 @@ def test_c_host_programs(T, dm, blocks, tmp_path):
         for b in want:
             fnv = ((fnv ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
         assert int(got["fnv1a"], 16) == fnv, (w, h, q, ad)
+
+
+@pytest.mark.parametrize("prog", ["dct", "quantization", "entropy"])
+def test_reference_programs_relinked(T, dm, prog):
+    """Drop-in check: the reference's OWN test programs (tests/test_<prog>.c, with
+    the reference's headers), linked against libdct_amd.so in place of
+    src/{utils,dct,quantization}.c, print exactly what they print when linked
+    against the reference (tests/golden/ref_programs.json) and exit 0.  The
+    binaries are built by oracle/Makefile where /root/reference exists and
+    travel to the GPU box as built files (oracle/_ref/)."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "oracle", "_ref", f"test_{prog}_amd")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/test_*_amd not built (needs /root/reference at build time)")
+    want = json.load(open(os.path.join(root, "tests", "golden", "ref_programs.json")))[prog]
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == want["rc"], r.stderr
+    assert r.stdout == want["stdout"]

@@ -118,3 +118,19 @@ def test_synth_kinds_are_distinct():
     assert set(np.unique(a[3])) <= {0, 255}
     c = a[2].reshape(8, 8, 8, 8).transpose(0, 2, 1, 3).reshape(64, 64)
     assert (c == c[:, :1]).all()  # constant 8x8 blocks
+
+
+def test_reference_programs_golden():
+    """The committed expected output of the reference's own test programs is what
+    they print here, linked against the reference (oracle/_ref/test_*_cpu)."""
+    import json
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    want = json.load(open(os.path.join(root, "tests", "golden", "ref_programs.json")))
+    for prog, w in want.items():
+        exe = os.path.join(root, "oracle", "_ref", f"test_{prog}_cpu")
+        if not os.path.exists(exe):
+            pytest.skip("oracle/_ref/test_*_cpu not built (needs /root/reference)")
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+        assert (r.returncode, r.stdout) == (w["rc"], w["stdout"]), prog

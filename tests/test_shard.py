@@ -1,0 +1,82 @@
+"""CPU, world_size 2 and 3 over gloo: the multi-GPU partitioning (dct_amd/shard.py).
+
+Each rank transforms only its shard -- here with the oracle standing in for
+the device kernel, since this container has no GPU (the -m gpu tests prove the
+kernel equals the oracle) -- then the coefficient shards are all-gathered and
+every rank checks the result equals the unsharded plane's coefficients in the
+reference's raster block order."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dct_amd import shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # (1) frame shards of a ragged batch: 5 frames of 48x40
+        frames = torch.from_numpy(np.stack([O.synth_plane(7 + f, O.KINDS["uniform"], 48, 40) for f in range(5)]))
+        mine, (lo, hi) = shard.frame_shard(frames, world, rank)
+        local = torch.from_numpy(np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in mine])
+                                 if hi > lo else np.zeros((0, 64), np.int16))
+        per = (48 // 8) * (40 // 8)
+        counts = [(shard.split(5, world, r)[1] - shard.split(5, world, r)[0]) * per for r in range(world)]
+        full = shard.gather_coefficients(local, counts)
+        want = np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in frames])
+        assert np.array_equal(full.numpy(), want), "frame-sharded gather differs"
+
+        # (2) block-row bands of one plane: 7 block rows, adaptive, q90
+        plane = torch.from_numpy(O.synth_plane(99, O.KINDS["smooth"], 64, 56))
+        band, (row0, rows) = shard.band_shard(plane, world, rank)
+        local = torch.from_numpy(O.forward_plane(np.ascontiguousarray(band.numpy()), 90, 1)
+                                 if rows else np.zeros((0, 64), np.int16))
+        counts = [shard.split(7, world, r)[1] * 8 - shard.split(7, world, r)[0] * 8 for r in range(world)]
+        full = shard.gather_coefficients(local, counts)
+        assert np.array_equal(full.numpy(), O.forward_plane(plane.numpy(), 90, 1)), "band-sharded gather differs"
+        q.put((rank, "ok"))
+    except BaseException as e:  # noqa: BLE001 -- report to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_gather_matches_unsharded(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {r: "ok" for r in range(world)}, res
+
+
+def test_split_covers_exactly():
+    for n in [0, 1, 7, 64, 270, 1000]:
+        for world in [1, 2, 3, 8]:
+            parts = [shard.split(n, world, r) for r in range(world)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            sizes = [hi - lo for lo, hi in parts]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard.split(4, 2, 2)
