@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
+    ap.add_argument("--backend", default="nccl", help="N>1 process group (nccl = RCCL; gloo only to rehearse "
+                                                      "several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -112,7 +114,8 @@ def gather_leg(args, plan, luma, coef_y, world, rank, dev):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     ok = bool(torch.equal(full[rank * n:(rank + 1) * n], coef_y))
-    return {"op": "forward_quant(luma) + all_gather_into_tensor (RCCL) of int16 coefficient planes",
+    be = "RCCL all_gather_into_tensor" if dist.get_backend() == "nccl" else f"{dist.get_backend()} all_gather"
+    return {"op": f"forward_quant(luma) + {be} of int16 coefficient planes",
             "blocks_per_s": world * n * args.gather_steps / el, "ms_per_step": el / args.gather_steps * 1e3,
             "bytes_received_per_rank": (world - 1) * n * 128, "steps": args.gather_steps,
             "own_slice_intact": ok}
@@ -124,8 +127,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share a GPU
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
     F = args.frames

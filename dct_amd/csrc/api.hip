@@ -162,9 +162,37 @@ static int plane_args(const dctq_plane *s, dctq::PlaneArgs *a) {
     return DCTQ_OK;
 }
 
+
+namespace dctq {
+namespace {
+std::recursive_mutex g_rand_mu;
+char g_rand_state[256];  // the runtime's private rand() state, persists across calls
+int g_rand_depth = 0;
+bool g_rand_init = false;
+}  // namespace
+
+RandIsolation::RandIsolation() : saved_(nullptr) {
+    g_rand_mu.lock();
+    if (g_rand_depth++ == 0) {
+        if (!g_rand_init) {
+            saved_ = initstate(1u, g_rand_state, sizeof g_rand_state);
+            g_rand_init = true;
+        } else {
+            saved_ = setstate(g_rand_state);
+        }
+    }
+}
+
+RandIsolation::~RandIsolation() {
+    if (--g_rand_depth == 0) setstate(saved_);
+    g_rand_mu.unlock();
+}
+}  // namespace dctq
+
 extern "C" {
 
 int dctq_plan_create(int quality, int adaptive, dctq_plan **plan) {
+    DCTQ_ENTRY;
     double q[64];
     quality = dctq_host::clamp_quality(quality);
     dctq_host::quant_matrix(8, quality, q);
@@ -172,6 +200,7 @@ int dctq_plan_create(int quality, int adaptive, dctq_plan **plan) {
 }
 
 int dctq_plan_from_context(const QuantContext *qctx, dctq_plan **plan) {
+    DCTQ_ENTRY;
     if (!qctx || qctx->block_size != 8 || !qctx->quant_matrix) return fail(DCTQ_EINVAL, "QuantContext must be 8x8");
     double q[64];
     for (int i = 0; i < 8; ++i)
@@ -180,6 +209,7 @@ int dctq_plan_from_context(const QuantContext *qctx, dctq_plan **plan) {
 }
 
 void dctq_plan_destroy(dctq_plan *plan) {
+    DCTQ_ENTRY;
     if (!plan) return;
     (void)hipFree(plan->dev);
     (void)hipFree(plan->ring);
@@ -187,12 +217,14 @@ void dctq_plan_destroy(dctq_plan *plan) {
 }
 
 int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter) {
+    DCTQ_ENTRY;
     if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
     plan->fallbacks = counter;
     return DCTQ_OK;
 }
 
 int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num, void *stream) {
+    DCTQ_ENTRY;
     if (!plan || !coef) return fail(DCTQ_EINVAL, "plan/coef is NULL");
     if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
     dctq::PlaneArgs a;
@@ -206,6 +238,7 @@ int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *co
 }
 
 int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream) {
+    DCTQ_ENTRY;
     if (!plan || !coef) return fail(DCTQ_EINVAL, "plan/coef is NULL");
     if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
     dctq::PlaneArgs a;
@@ -217,6 +250,7 @@ int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef
 
 int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks, float *recon,
                  void *stream) {
+    DCTQ_ENTRY;
     if (!plan || !coef || !recon) return fail(DCTQ_EINVAL, "plan/coef/recon is NULL");
     if (plan->adaptive && !var_num) return fail(DCTQ_EINVAL, "adaptive inverse needs var_num");
     if (nblocks < 0 || nblocks >= (1ll << 40)) return fail(DCTQ_EINVAL, "bad nblocks");
@@ -228,6 +262,7 @@ int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_
 }
 
 int dctq_synth(uint64_t seed, int kind, const dctq_plane *dst, void *stream) {
+    DCTQ_ENTRY;
     if (!dst || !dst->pixels) return fail(DCTQ_EINVAL, "dst is NULL");
     if (dst->width <= 0 || dst->height <= 0 || dst->width % 4 || dst->stride < dst->width || dst->stride % 4 ||
         dst->nframes < 1 || ((uintptr_t)dst->pixels) % 4)
@@ -239,30 +274,37 @@ int dctq_synth(uint64_t seed, int kind, const dctq_plane *dst, void *stream) {
 }
 
 int dctq_device_count(int *count) {
+    DCTQ_ENTRY;
     HIPCHK(hipGetDeviceCount(count), "hipGetDeviceCount");
     return DCTQ_OK;
 }
 int dctq_set_device(int device) {
+    DCTQ_ENTRY;
     HIPCHK(hipSetDevice(device), "hipSetDevice");
     return DCTQ_OK;
 }
 int dctq_malloc(void **ptr, size_t bytes) {
+    DCTQ_ENTRY;
     HIPCHK(hipMalloc(ptr, bytes), "hipMalloc");
     return DCTQ_OK;
 }
 int dctq_free(void *ptr) {
+    DCTQ_ENTRY;
     HIPCHK(hipFree(ptr), "hipFree");
     return DCTQ_OK;
 }
 int dctq_memcpy_htod(void *dst, const void *src, size_t bytes) {
+    DCTQ_ENTRY;
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
     return DCTQ_OK;
 }
 int dctq_memcpy_dtoh(void *dst, const void *src, size_t bytes) {
+    DCTQ_ENTRY;
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
     return DCTQ_OK;
 }
 int dctq_synchronize(void *stream) {
+    DCTQ_ENTRY;
     HIPCHK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
     return DCTQ_OK;
 }

@@ -5,6 +5,26 @@
 
 namespace dctq {
 
+// The HSA runtime calls srand()/rand() (libhsa-runtime64 imports both), which
+// would reseed or advance the HOST APPLICATION's rand() stream; the reference's
+// own tests draw their blocks from rand() (tests/test_quantization.c:127,134).
+// Every exported entry point holds one of these while it may reach the HIP
+// runtime: glibc's global random state is swapped to a private one for the
+// duration (initstate/setstate keep the caller's state and position intact).
+// Entry points are serialised by it (recursive, so nesting is fine).
+class RandIsolation {
+  public:
+    RandIsolation();
+    ~RandIsolation();
+    RandIsolation(const RandIsolation &) = delete;
+    RandIsolation &operator=(const RandIsolation &) = delete;
+
+  private:
+    char *saved_;
+};
+#define DCTQ_ENTRY ::dctq::RandIsolation dctq_rand_isolation_
+
+
 // n / d and n % d by multiply-high, valid for 0 <= n < 2^31 (host-built magic).
 struct FastDiv {
     uint32_t d, m, s;

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "dct.h"
+#include "dctq_internal.h"
 #include "host_tables.h"
 #include "quantization.h"
 #include "utils.h"
@@ -155,6 +156,7 @@ void check_n(int n) {
 }
 
 void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
+    DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int n = ctx->block_size, nn = n * n;
     check_n(n);
     const size_t bytes = sizeof(double) * 3 * nn;
@@ -176,6 +178,7 @@ void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
 // One elementwise launch over an n x n block; inputs/outputs as flat host arrays.
 void elementwise(int mode, int n, double **m, int flag, double variance, const double *din, const int *iin,
                  double *dout, int *iout) {
+    DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int nn = n * n;
     const size_t bytes = sizeof(double) * 3 * nn + sizeof(int) * 2 * nn;
     unsigned char *dev = (unsigned char *)g_stage.get(bytes);
@@ -339,6 +342,7 @@ void dequantize(QuantContext *ctx, int **quant_coeffs, double **dct_coeffs, doub
 }
 
 double calculate_block_variance(double **block, int block_size) {
+    DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     check_n(block_size);
     const int nn = block_size * block_size;
     double *dev = (double *)g_stage.get(sizeof(double) * (nn + 1));

@@ -30,6 +30,7 @@ for step in "$@"; do
     pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
     pmcsq) run pmcsq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
     pmcsq2) run pmcsq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU -d $OUT/pmc_sq2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --frames 16 --no-cpu --backend gloo ;;
     list) run list 120 rocprofv3 -L ;;
     traffic) run traffic 60 bash -c "python tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv --frames 64 --kind uniform -o $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic.json" ;;
     ablate) run ablate 300 python tools/ablate_bench.py ;;
