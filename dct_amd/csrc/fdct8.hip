@@ -270,8 +270,15 @@ typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 constexpr int kQCap = 128;     // per-wave tie queue: < 64 between rounds + one round of <= 64
 constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) conflicts for the b32 writes
+#ifndef DCTQ_STORE_AUX
+// Cache policy of the bulk coefficient stores (gfx950: 1 sc0, 2 nt, 16 sc1).
+// Non-temporal: -15 % kernel time on the 4K stream (profiles/r01/store_policy.md);
+// the written lines are never re-read by this kernel except by tie patches,
+// which come after a vmcnt(0).
+#define DCTQ_STORE_AUX 2
+#endif
 #ifndef DCTQ_ABLATE
-#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run
+#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores
 #endif
 
 template <int K>
@@ -287,6 +294,15 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
 // Pixel rows are read exactly once: non-temporal loads (+8.7 % on the memory
 // ceiling of this stream, profiles/r01/valu_issue_rates.md).
 __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 (&rows)[8]) {
+    if (DCTQ_ABLATE & 64) {  // diagnostic: opaque synthetic rows, no memory traffic
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            uint32_t a = n * 0x9E3779B1u + r, c = a ^ (a >> 13);
+            asm volatile("" : "+v"(a), "+v"(c));
+            rows[r] = make_uint2(a, c);
+        }
+        return;
+    }
     const uint8_t *px = block_ptr(p, n < (uint32_t)p.nblk ? n : 0);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -366,21 +382,14 @@ __device__ __forceinline__ void drain_queue(const DevTables *__restrict__ dev, i
     __builtin_amdgcn_s_waitcnt(0x0F70);  // nothing of this rare path stays in flight
 }
 
-// One 64-block batch of the v2 loop.  `nxt` holds this batch's rows on entry and
-// the next batch's rows on exit.
-template <bool ADAPTIVE, bool VAR, bool STATS>
-__device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables *__restrict__ dev,
-                                            int16_t *__restrict__ coef, int32_t *__restrict__ var_out,
-                                            unsigned long long *fallbacks, uint4 *stage, uint32_t *q, uint4 *ring,
-                                            int &qn, uint2 (&nxt)[8], uint32_t b, uint32_t step, int lane, int wv) {
+// The arithmetic of one 64-block batch (one block per lane): u8 rows -> fp32,
+// exact variance numerator, AAN row pass, column pairs fused with quantization
+// into the wave's LDS stage, tie masks (bit 31 - p%32 of mlo/mhi = processing
+// slot p = 16*cp + 2*i + h needs the exact path).
+template <bool ADAPTIVE, bool VAR>
+__device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev, const uint2 (&cur)[8], uint4 *stage,
+                                              int lane, int wv, uint32_t &mlo, uint32_t &mhi, int32_t &var_num) {
     const f2 M2 = {kMagic, kMagic};
-    uint2 cur[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-    const uint32_t n = b * 64 + lane;
-    const bool valid = n < (uint32_t)p.nblk;
-    load_rows(p, (b + step) * 64 + lane, nxt);  // unconditional: past the end it re-reads block 0
-
     float v[8][8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -393,7 +402,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
         v[r][6] = cvt_ubyte<2>(cur[r].y);
         v[r][7] = cvt_ubyte<3>(cur[r].y);
     }
-    int32_t var_num = 0;
+    var_num = 0;
     if (ADAPTIVE || VAR) {
         uint32_t s1 = 0, s2 = 0;
 #pragma unroll
@@ -426,7 +435,8 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
     const FastTables *tg = &dev->fast;
     asm volatile("" : "+s"(tg));
     const __attribute__((address_space(4))) FastTables *tp = (const __attribute__((address_space(4))) FastTables *)tg;
-    uint32_t mlo = 0, mhi = 0;  // bit (31 - p%32): processing slot p = 16*cp + 2*i + h flagged
+    mlo = 0;
+    mhi = 0;  // bit (31 - p%32): processing slot p = 16*cp + 2*i + h flagged
     uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
 #pragma unroll
     for (int cp = 0; cp < 4; ++cp) {
@@ -467,6 +477,25 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
         // and keeps every residual live across the stores.
         asm volatile("" : "+v"(mlo), "+v"(mhi));
     }
+}
+
+// One 64-block batch of the v2 loop.  `nxt` holds this batch's rows on entry and
+// the next batch's rows on exit.
+template <bool ADAPTIVE, bool VAR, bool STATS>
+__device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables *__restrict__ dev,
+                                            int16_t *__restrict__ coef, int32_t *__restrict__ var_out,
+                                            unsigned long long *fallbacks, uint4 *stage, uint32_t *q, uint4 *ring,
+                                            int &qn, uint2 (&nxt)[8], uint32_t b, uint32_t step, int lane, int wv) {
+    uint2 cur[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+    const uint32_t n = b * 64 + lane;
+    const bool valid = n < (uint32_t)p.nblk;
+    load_rows(p, (b + step) * 64 + lane, nxt);  // unconditional: past the end it re-reads block 0
+
+    uint32_t mlo, mhi;
+    int32_t var_num;
+    fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
 
     // Consume the prefetched rows HERE, before this batch's stores are issued:
     // the wait the compiler puts in front of this fence then covers loads issued
@@ -501,12 +530,17 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
             const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
             val[k] = u4v{lo.x, lo.y, hi.x, hi.y};
         }
+        if (DCTQ_ABLATE & 128) {  // diagnostic: consume the staged values, store nothing
 #pragma unroll
-        for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, 0);
+            for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(val[k]));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_STORE_AUX);
+        }
         if (VAR) {
             const __amdgpu_buffer_rsrc_t rv =
                 __builtin_amdgcn_make_buffer_rsrc(var_out + (size_t)b * 64, (short)0, (int)(nb * 4u), 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_STORE_AUX);
         }
     }
 
@@ -577,6 +611,7 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneArgs p, FastT
     if (DCTQ_ABLATE & 16) qn = 0;
     while (qn > 0) drain_queue<ADAPTIVE, STATS>(dev, coef, q, ring, qn, lane, fallbacks);
 }
+
 
 #define DCTQ_SELECT(KERN, A, V, S, ...)                                          \
     do {                                                                         \

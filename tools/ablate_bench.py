@@ -13,10 +13,16 @@ sys.path.insert(0, ROOT)
 import dct_amd  # noqa: E402
 
 libs = {"full": dct_amd.LIB_PATH}
-for m, name in [(8, "flags-no-queue"), (16, "append-no-drain"), (32, "queue-code-idle")]:
+NAMES = {1: "no-tie-flags", 2: "no-butterfly", 8: "flags-no-queue", 16: "append-no-drain", 32: "queue-code-idle",
+         64: "no-pixel-loads", 128: "no-coef-stores", 192: "no-loads-no-stores", 194: "no-mem-no-butterfly"}
+for m, name in sorted(NAMES.items()):
     p = os.path.join(ROOT, "tools", "ubench", f"libablate_{m}.so")
     if os.path.exists(p):
         libs[name] = p
+for a in (1, 2, 3, 16, 17):  # store cache-policy builds (tools/ubench/policy.sh)
+    p = os.path.join(ROOT, "tools", "ubench", f"libpolicy_{a}.so")
+    if os.path.exists(p):
+        libs[f"store-aux-{a}"] = p
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 px = dct_amd.synth(7, "uniform", 3840, 2160, F)
 d = dct_amd.plane_desc(px)

@@ -38,6 +38,11 @@ for step in "$@"; do
     pmcv2d) run pmcv2d 600 rocprofv3 --pmc TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum -d $OUT/pmc_v2d -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
     pmcv2) run pmcv2 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_v2 -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
     pmcv2b) run pmcv2b 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA -d $OUT/pmc_v2b -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
+    abb) run abb 300 python tools/ab_bench.py --variants 2 --b2b 20 ;;
+    ceil) run ceil 120 tools/ubench/stream_ceiling ;;
+    clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
+    ab23) run ab23 300 bash -c "python tools/ab_bench.py --variants 2,3 --rounds 12 && python tools/ab_bench.py --variants 2,3 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3 --rounds 6 --kind const && python tools/ab_bench.py --variants 2,3 --rounds 6 --adaptive 1 && python tools/ab_bench.py --variants 2,3 --rounds 6 --quality 90" ;;
+    ab234) run ab234 300 bash -c "python tools/ab_bench.py --variants 2,3,4 --rounds 12 && python tools/ab_bench.py --variants 2,3,4 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3,4 --rounds 6 --kind const" ;;
     ab) run ab 300 python tools/ab_bench.py --variants 1,2 ;;
     abk) run abk 300 bash -c "python tools/ab_bench.py --kind smooth && python tools/ab_bench.py --kind const && python tools/ab_bench.py --adaptive 1 && python tools/ab_bench.py --quality 90" ;;
     *) echo "unknown step $step"; exit 2 ;;
