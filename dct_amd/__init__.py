@@ -52,6 +52,7 @@ def lib() -> C.CDLL:
             "dctq_error_string": ([i], C.c_char_p),
             "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
             "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
+            "dctq_debug_dc_table": ([i, vp], i),
             "dctq_synchronize": ([vp], i),
         }
         for name, (args, res) in sig.items():

@@ -89,6 +89,21 @@ void fill_fast_tables(const double *q, int adaptive, FastTables *t) {
 }
 }  // namespace dctq
 
+// Quantized DC of a constant block, exactly as the reference computes it:
+// temp[k][0] = sum_l x * D[0][l] (the same for every row k, l ascending), then
+// out = sum_k D[0][k] * temp[k][0], q = (int) round(out / Q[0]).  This file is
+// compiled with -ffp-contract=off, so host arithmetic is the reference's.
+static void dc_const_table(const double *d, const double *q, int16_t *tab) {
+    for (int v = 0; v < 256; ++v) {
+        const double x = (double)v - 128.0;
+        double t = 0.0;
+        for (int l = 0; l < 8; ++l) t += x * d[l];
+        double out = 0.0;
+        for (int k = 0; k < 8; ++k) out += d[k] * t;
+        tab[v] = (int16_t)(int)round(out / q[0]);
+    }
+}
+
 static int build_plan(const double *q, int quality, int adaptive, dctq_plan **out) {
     if (!out) return fail(DCTQ_EINVAL, "plan pointer is NULL");
     for (int c = 0; c < 64; ++c)
@@ -117,6 +132,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
         p->host.qscale[c] = q[c] * s2;
     }
     dctq::fill_fast_tables(q, p->adaptive, &p->fast);
+    dc_const_table(p->host.dct, p->host.quant, p->host.dc_const);
     p->host.fast = p->fast;
     hipError_t e = hipMalloc(&p->dev, sizeof(dctq::DevTables));
     if (e != hipSuccess) {
@@ -332,6 +348,14 @@ int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *d
     if (thr) memcpy(thr, t.thr, sizeof t.thr);
     if (dct) dctq_host::dct_matrix(8, dct);
     if (quant) memcpy(quant, q, sizeof q);
+    return DCTQ_OK;
+}
+
+int dctq_debug_dc_table(int quality, int16_t *out) {
+    double d[64], q[64];
+    dctq_host::dct_matrix(8, d);
+    dctq_host::quant_matrix(8, dctq_host::clamp_quality(quality), q);
+    dc_const_table(d, q, out);
     return DCTQ_OK;
 }
 

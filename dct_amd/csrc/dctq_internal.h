@@ -51,6 +51,11 @@ struct DevTables {
     double qscale[64]; // inverse path (adaptive): Q * S_i S_j
     double s2[64];     // S_i S_j
     FastTables fast;   // device copy of the fast-path tables (v2 reads them per batch)
+    // quantized DC of a CONSTANT block of centred value v-128, computed on the
+    // host in the reference's order (src/dct.c:57-74, src/quantization.c:124):
+    // resolves the DC ties of flat blocks without the exact path.  The DC is
+    // never adjusted by adaptive plans (src/quantization.c:198-199).
+    int16_t dc_const[256];
 };
 
 struct PlaneArgs {

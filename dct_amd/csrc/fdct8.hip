@@ -497,6 +497,21 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
     int32_t var_num;
     fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
 
+    // A flagged DC of a CONSTANT block (flat image areas: an exact .5 tie for
+    // half of all pixel values at q50) is resolved from the plan's table of
+    // reference-order DCs instead of the exact path.  Checked only when some
+    // lane's DC (processing slot 0 = bit 31 of mlo) is flagged.
+    if (!(DCTQ_ABLATE & 8) && __builtin_amdgcn_ballot_w64((mlo >> 31) != 0u)) {
+        const uint32_t w = cur[0].x;
+        bool flat = w == (w & 0xFFu) * 0x01010101u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) flat = flat && cur[r].x == w && cur[r].y == w;
+        if ((mlo >> 31) && flat) {
+            reinterpret_cast<int16_t *>(stage)[(wv * 64 + lane) * (kPitch2 / 2)] = dev->dc_const[w & 0xFFu];
+            mlo &= 0x7FFFFFFFu;
+        }
+    }
+
     // Consume the prefetched rows HERE, before this batch's stores are issued:
     // the wait the compiler puts in front of this fence then covers loads issued
     // a whole compute phase ago and nothing younger.  Left to itself it waits at

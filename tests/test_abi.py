@@ -118,3 +118,18 @@ int main(void){
         assert res["ours"].split() == ["24", "0", "8", "16", "32", "0", "4", "8", "16", "24"]
         if "ref" in res:
             assert res["ours"] == res["ref"]
+
+
+def test_constant_block_dc_table(lib):
+    """The per-plan table of quantized DCs of constant blocks (flat-block tie
+    resolution in the forward kernel) equals the oracle's reference-order
+    forward + quantize of each constant block."""
+    import oracle as O
+    for q in [1, 10, 25, 50, 75, 90, 100]:
+        tab = np.zeros(256, np.int16)
+        assert lib.dctq_debug_dc_table(q, tab.ctypes.data) == 0
+        for v in range(256):
+            x = np.full((8, 8), v - 128.0)
+            want = O.quantize(O.forward(x), q, 0, 0.0)[0, 0]
+            assert tab[v] == want, (q, v, tab[v], want)
+            assert O.quantize(O.forward(x), q, 1, O.variance(x))[0, 0] == want  # adaptive keeps Q for the DC

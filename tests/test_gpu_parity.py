@@ -142,18 +142,37 @@ def test_var_num_exact(T, dm, tiles):
 
 
 def test_fallback_counter_and_exactness(T, dm):
-    """Constant blocks at q50 tie at DC in half of the blocks: the exact path runs."""
+    """Ties are resolved exactly, and the fallback counter sees the exact path run.
+
+    * constant 8x8 blocks at q50: the DC is an exact .5 tie for half of them; the
+      kernel resolves those from the plan's constant-block DC table, so the exact
+      path never runs (counter 0) and the output is still the reference's;
+    * left/right step blocks (a|b) at q50: DC/Q = (a+b)/4 - 64 ties whenever
+      a+b = 2 mod 4 (a quarter of the blocks) and the blocks are not flat, so
+      those DCs go through the exact fp64 path."""
     import oracle as O
-    px = O.synth_plane(9, 2, 1024, 512)
-    cnt = T.zeros(1, dtype=T.int64, device="cuda")
     plan = dm.Plan(50, 0)
+    cnt = T.zeros(1, dtype=T.int64, device="cuda")
     plan.set_fallback_counter(cnt)
+
+    px = O.synth_plane(9, 2, 1024, 512)
+    got = plan.forward_quant(gpu_px(T, px)).cpu().numpy()
+    assert np.array_equal(got, O.forward_plane(px, 50, 0))
+    assert int(cnt.item()) == 0
+
+    rng = np.random.default_rng(5)
+    by, bx = 64, 128
+    ab = rng.integers(0, 256, (by, bx, 2), dtype=np.uint8)
+    blk = np.concatenate([np.repeat(ab[:, :, :1, None], 4, 3).repeat(8, 2),
+                          np.repeat(ab[:, :, 1:, None], 4, 3).repeat(8, 2)], axis=3)  # [by, bx, 8, 8]
+    px = np.ascontiguousarray(blk.transpose(0, 2, 1, 3).reshape(by * 8, bx * 8))
     got = plan.forward_quant(gpu_px(T, px)).cpu().numpy()
     plan.set_fallback_counter(None)
     assert np.array_equal(got, O.forward_plane(px, 50, 0))
+    a, b = ab[:, :, 0].astype(int), ab[:, :, 1].astype(int)
+    ties = int(((((a + b) % 4) == 2) & (a != b)).sum())  # a == b blocks are flat: table, not exact path
     n = int(cnt.item())
-    nblk = px.size // 64
-    assert 0.3 * nblk < n < 0.7 * nblk, n
+    assert ties <= n < ties + 0.05 * by * bx, (n, ties)
 
 
 def test_forward_float_tolerance(T, dm, tiles):
