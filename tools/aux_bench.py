@@ -1,0 +1,39 @@
+"""Time the non-quantizing kernels (forward_float, inverse) on 64 x 4K luma
+planes, interleaved, HIP events per launch; report % of 8 TB/s on algorithmic bytes."""
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import dct_amd  # noqa: E402
+
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+W, H = 3840, 2160
+nblk = F * (W // 8) * (H // 8)
+px = dct_amd.synth(7, "uniform", W, H, F)
+res = {}
+for ad in (0, 1):
+    plan = dct_amd.Plan(50, ad)
+    vn = torch.empty(nblk, dtype=torch.int32, device="cuda")
+    coef = plan.forward_quant(px, var_num=vn)
+    ff = torch.empty((nblk, 64), dtype=torch.float32, device="cuda")
+    rec = torch.empty((nblk, 64), dtype=torch.float32, device="cuda")
+    jobs = {f"forward_float a{ad}": (lambda: plan.forward_float(px, out=ff), 64 + 256),
+            f"inverse a{ad}": (lambda: plan.inverse(coef, var_num=vn, out=rec), 128 + 256 + (4 if ad else 0)),
+            f"forward_quant+var a{ad}": (lambda: plan.forward_quant(px, out=coef, var_num=vn), 64 + 128 + 4)}
+    for name, (fn, bpb) in jobs.items():
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(8):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e-3)
+        med = statistics.median(ts)
+        print(f"{name:24s} median {med*1e6:8.1f} us  {nblk/med/1e9:6.2f} Gblk/s  {nblk*bpb/med/1e9:6.0f} GB/s "
+              f"({nblk*bpb/med/8e12*100:5.1f}% of 8 TB/s, {bpb} B/block)")

@@ -41,6 +41,7 @@ for step in "$@"; do
     abb) run abb 300 python tools/ab_bench.py --variants 2 --b2b 20 ;;
     ceil) run ceil 120 tools/ubench/stream_ceiling ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
+    aux) run aux 300 python tools/aux_bench.py ;;
     ab23) run ab23 300 bash -c "python tools/ab_bench.py --variants 2,3 --rounds 12 && python tools/ab_bench.py --variants 2,3 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3 --rounds 6 --kind const && python tools/ab_bench.py --variants 2,3 --rounds 6 --adaptive 1 && python tools/ab_bench.py --variants 2,3 --rounds 6 --quality 90" ;;
     ab234) run ab234 300 bash -c "python tools/ab_bench.py --variants 2,3,4 --rounds 12 && python tools/ab_bench.py --variants 2,3,4 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3,4 --rounds 6 --kind const" ;;
     ab) run ab 300 python tools/ab_bench.py --variants 1,2 ;;
