@@ -133,6 +133,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
     }
     dctq::fill_fast_tables(q, p->adaptive, &p->fast);
     dc_const_table(p->host.dct, p->host.quant, p->host.dc_const);
+    for (int k = 0; k < 8; ++k) p->host.s1[k] = kAanScale[k];
     p->host.fast = p->fast;
     hipError_t e = hipMalloc(&p->dev, sizeof(dctq::DevTables));
     if (e != hipSuccess) {
@@ -260,7 +261,11 @@ int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef
     dctq::PlaneArgs a;
     int rc = plane_args(src, &a);
     if (rc) return rc;
-    HIPCHK(dctq::launch_fdct8_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
+    if (plan->variant == 1)
+        HIPCHK(dctq::launch_fdct8_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
+    else
+        HIPCHK(dctq::launch_fdct8_float_pair(a, plan->dev, coef, (hipStream_t)stream, plan->num_cus),
+               "fdct8_float_pair launch");
     return DCTQ_OK;
 }
 
@@ -272,8 +277,13 @@ int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_
     if (nblocks < 0 || nblocks >= (1ll << 40)) return fail(DCTQ_EINVAL, "bad nblocks");
     if (((uintptr_t)coef) % 16 || ((uintptr_t)recon) % 16) return fail(DCTQ_EINVAL, "coef/recon must be 16-byte aligned");
     if (nblocks == 0) return DCTQ_OK;
-    HIPCHK(dctq::launch_idct8(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream),
-           "idct8 launch");
+    if (plan->variant == 1)
+        HIPCHK(dctq::launch_idct8(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream),
+               "idct8 launch");
+    else
+        HIPCHK(dctq::launch_idct8_pair(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream,
+                                       plan->num_cus),
+               "idct8_pair launch");
     return DCTQ_OK;
 }
 

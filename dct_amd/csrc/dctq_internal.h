@@ -50,6 +50,7 @@ struct DevTables {
     double iscale[64]; // inverse path: 1/Q * S_i S_j (non-adaptive dequant folded with AAN^T scale)
     double qscale[64]; // inverse path (adaptive): Q * S_i S_j
     double s2[64];     // S_i S_j
+    double s1[8];      // S_k: AAN output scale X_k = S_k y_k (per-slot factors of the paired fp64 kernels)
     FastTables fast;   // device copy of the fast-path tables (v2 reads them per batch)
     // quantized DC of a CONSTANT block of centred value v-128, computed on the
     // host in the reference's order (src/dct.c:57-74, src/quantization.c:124):
@@ -72,6 +73,10 @@ hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const Dev
                               hipStream_t stream, int variant, int num_cus, void *ring, int ring_wgs);
 // bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
 size_t fdct8_ring_bytes(int workgroups);
+hipError_t launch_fdct8_float_pair(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream,
+                                   int num_cus);
+hipError_t launch_idct8_pair(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
+                             long long nblk, float *recon, hipStream_t stream, int num_cus);
 hipError_t launch_fdct8_float(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);
 hipError_t launch_idct8(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
                         long long nblk, float *recon, hipStream_t stream);

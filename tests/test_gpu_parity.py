@@ -198,6 +198,32 @@ def test_inverse_round_trip(T, dm):
             assert np.abs(rec - want).max() <= 1e-4, (kind, q, ad, np.abs(rec - want).max())
 
 
+def test_float_and_inverse_ragged_geometries(T, dm):
+    """The fp64 kernels process 32 blocks per wave (two lanes per block): block
+    counts that are not multiples of 32, multi-frame stacks and padded rows."""
+    import oracle as O
+    for (w, h, nf, pad) in [(8, 8, 1, 0), (40, 24, 1, 0), (264, 8, 1, 8), (136, 56, 3, 16), (1920, 16, 2, 0)]:
+        frames = [O.synth_plane(70 + f, O.KINDS["uniform"], w, h) for f in range(nf)]
+        buf = np.zeros((nf, h, w + pad), np.uint8)
+        for f in range(nf):
+            buf[f, :, :w] = frames[f]
+        g = T.from_numpy(buf).cuda()[:, :, :w]
+        for q, ad in [(50, 0), (75, 1)]:
+            plan = dm.Plan(q, ad)
+            ff = plan.forward_float(g).cpu().numpy().astype(np.float64)
+            want_f = np.concatenate([O.forward_plane(fr, q, ad, want_float=True)[1].reshape(-1, 64) for fr in frames])
+            assert np.abs(ff - want_f).max() <= 1e-4, (w, h, nf, q, ad)
+            vn = T.zeros(nf * (w // 8) * (h // 8), dtype=T.int32, device="cuda")
+            coef = plan.forward_quant(g, var_num=vn)
+            rec = plan.inverse(coef, var_num=vn).cpu().numpy().astype(np.float64)
+            c = coef.cpu().numpy()
+            per = (w // 8) * (h // 8)
+            want = np.concatenate([
+                O.inverse_plane(c[f * per:(f + 1) * per], q, ad, O.plane_variance(frames[f]) if ad else None)
+                for f in range(nf)]) + 128.0
+            assert np.abs(rec - want).max() <= 1e-4, (w, h, nf, q, ad)
+
+
 def test_example_block_pipeline(T, dm, blocks):
     """tests/test_entropy.c:290-393 example block through the batched API."""
     from golden.make_golden import EXAMPLE

@@ -14,15 +14,17 @@ W, H = 3840, 2160
 nblk = F * (W // 8) * (H // 8)
 px = dct_amd.synth(7, "uniform", W, H, F)
 res = {}
-for ad in (0, 1):
+for var, ad in [(v, a) for a in (0, 1) for v in ("1", "2")]:
+    os.environ["DCTQ_FDCT_VARIANT"] = var
     plan = dct_amd.Plan(50, ad)
     vn = torch.empty(nblk, dtype=torch.int32, device="cuda")
     coef = plan.forward_quant(px, var_num=vn)
     ff = torch.empty((nblk, 64), dtype=torch.float32, device="cuda")
     rec = torch.empty((nblk, 64), dtype=torch.float32, device="cuda")
-    jobs = {f"forward_float a{ad}": (lambda: plan.forward_float(px, out=ff), 64 + 256),
-            f"inverse a{ad}": (lambda: plan.inverse(coef, var_num=vn, out=rec), 128 + 256 + (4 if ad else 0)),
-            f"forward_quant+var a{ad}": (lambda: plan.forward_quant(px, out=coef, var_num=vn), 64 + 128 + 4)}
+    jobs = {f"v{var} forward_float a{ad}": (lambda: plan.forward_float(px, out=ff), 64 + 256),
+            f"v{var} inverse a{ad}": (lambda: plan.inverse(coef, var_num=vn, out=rec), 128 + 256 + (4 if ad else 0))}
+    if var == "2":
+        jobs[f"v{var} forward_quant+var a{ad}"] = (lambda: plan.forward_quant(px, out=coef, var_num=vn), 64 + 128 + 4)
     for name, (fn, bpb) in jobs.items():
         fn()
         torch.cuda.synchronize()
@@ -35,5 +37,5 @@ for ad in (0, 1):
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1) * 1e-3)
         med = statistics.median(ts)
-        print(f"{name:24s} median {med*1e6:8.1f} us  {nblk/med/1e9:6.2f} Gblk/s  {nblk*bpb/med/1e9:6.0f} GB/s "
+        print(f"{name:27s} median {med*1e6:8.1f} us  {nblk/med/1e9:6.2f} Gblk/s  {nblk*bpb/med/1e9:6.0f} GB/s "
               f"({nblk*bpb/med/8e12*100:5.1f}% of 8 TB/s, {bpb} B/block)")
