@@ -277,6 +277,9 @@ constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) con
 // which come after a vmcnt(0).
 #define DCTQ_STORE_AUX 2
 #endif
+#ifndef DCTQ_LOAD_NT
+#define DCTQ_LOAD_NT 1  // pixel rows are read exactly once
+#endif
 #ifndef DCTQ_ABLATE
 #define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores
 #endif
@@ -306,8 +309,12 @@ __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 
     const uint8_t *px = block_ptr(p, n < (uint32_t)p.nblk ? n : 0);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
+#if DCTQ_LOAD_NT
         const u2v t = __builtin_nontemporal_load(reinterpret_cast<const u2v *>(px + r * p.stride));
         rows[r] = make_uint2(t.x, t.y);
+#else
+        rows[r] = *reinterpret_cast<const uint2 *>(px + r * p.stride);
+#endif
     }
 }
 

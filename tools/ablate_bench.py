@@ -19,10 +19,9 @@ for m, name in sorted(NAMES.items()):
     p = os.path.join(ROOT, "tools", "ubench", f"libablate_{m}.so")
     if os.path.exists(p):
         libs[name] = p
-for a in (1, 2, 3, 16, 17):  # store cache-policy builds (tools/ubench/policy.sh)
-    p = os.path.join(ROOT, "tools", "ubench", f"libpolicy_{a}.so")
-    if os.path.exists(p):
-        libs[f"store-aux-{a}"] = p
+import glob  # noqa: E402
+for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libpolicy_*.so"))):  # tools/ubench/policy.sh
+    libs["policy-" + os.path.basename(p)[len("libpolicy_"):-3]] = p
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 px = dct_amd.synth(7, "uniform", 3840, 2160, F)
 d = dct_amd.plane_desc(px)
