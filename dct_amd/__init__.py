@@ -54,6 +54,10 @@ def lib() -> C.CDLL:
             "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
             "dctq_debug_dc_table": ([i, vp], i),
             "dctq_synchronize": ([vp], i),
+            "dctq_rle_workspace_bytes": ([ll], C.c_size_t),
+            "dctq_rle_count": ([vp, ll, vp, vp, vp], i),
+            "dctq_rle_emit": ([vp, ll, vp, vp, vp], i),
+            "dctq_rle_decode": ([vp, vp, ll, vp, vp], i),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -145,6 +149,35 @@ class Plan:
                                   C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
                                   n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
         return out
+
+
+def rle_encode(coef, stream=None):
+    """Zigzag + run-length symbols of int16 blocks [N, 64] (src/entropy.c run_length_encode per
+    block, concatenated).  Returns (offsets [N+1], symbols [total]) as int32 tensors holding the
+    uint32 bit patterns: symbol = (uint16)value | run << 16.  Reads the total back (one sync)."""
+    import torch
+    n = coef.numel() // 64
+    ws = torch.empty(int(lib().dctq_rle_workspace_bytes(n)) // 4 + 1, dtype=torch.int32, device=coef.device)
+    off = torch.empty(n + 1, dtype=torch.int32, device=coef.device)
+    s = _stream_ptr(stream)
+    _check(lib().dctq_rle_count(C.c_void_p(coef.data_ptr()), n, C.c_void_p(off.data_ptr()),
+                                C.c_void_p(ws.data_ptr()), s))
+    total = int(off[n].item()) & 0xFFFFFFFF
+    sym = torch.empty(max(total, 1), dtype=torch.int32, device=coef.device)
+    _check(lib().dctq_rle_emit(C.c_void_p(coef.data_ptr()), n, C.c_void_p(off.data_ptr()),
+                               C.c_void_p(sym.data_ptr()), s))
+    return off, sym[:total]
+
+
+def rle_decode(symbols, offsets, out=None, stream=None):
+    """Inverse of rle_encode: int16 [N, 64] blocks (run_length_decode + zigzag_to_block)."""
+    import torch
+    n = offsets.numel() - 1
+    if out is None:
+        out = torch.empty((n, 64), dtype=torch.int16, device=offsets.device)
+    _check(lib().dctq_rle_decode(C.c_void_p(symbols.data_ptr()), C.c_void_p(offsets.data_ptr()), n,
+                                 C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    return out
 
 
 def synth(seed: int, kind, width: int, height: int, nframes: int = 1, device="cuda", stream=None, out=None):

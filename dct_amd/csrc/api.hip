@@ -299,6 +299,48 @@ int dctq_synth(uint64_t seed, int kind, const dctq_plane *dst, void *stream) {
     return DCTQ_OK;
 }
 
+static int device_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) return 256;
+    return n;
+}
+
+static int rle_args(const void *a, const void *b, long long nblocks) {
+    if (!a || !b) return fail(DCTQ_EINVAL, "NULL pointer");
+    if (nblocks < 1 || nblocks >= (1ll << 26)) return fail(DCTQ_EINVAL, "nblocks must be in [1, 2^26)");
+    return DCTQ_OK;
+}
+
+size_t dctq_rle_workspace_bytes(long long nblocks) { return dctq::rle_workspace_bytes(nblocks < 1 ? 1 : nblocks); }
+
+int dctq_rle_count(const int16_t *coef, long long nblocks, uint32_t *offsets, void *workspace, void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = rle_args(coef, offsets, nblocks)) return rc;
+    if (!workspace) return fail(DCTQ_EINVAL, "workspace is NULL");
+    HIPCHK(dctq::launch_rle_count(coef, nblocks, offsets, workspace, (hipStream_t)stream), "rle_count launch");
+    return DCTQ_OK;
+}
+
+int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offsets, uint32_t *symbols, void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = rle_args(coef, offsets, nblocks)) return rc;
+    if (!symbols) return fail(DCTQ_EINVAL, "symbols is NULL");
+    HIPCHK(dctq::launch_rle_emit(coef, nblocks, offsets, symbols, (hipStream_t)stream, device_cus()),
+           "rle_emit launch");
+    return DCTQ_OK;
+}
+
+int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
+                    void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = rle_args(symbols, offsets, nblocks)) return rc;
+    if (!coef) return fail(DCTQ_EINVAL, "coef is NULL");
+    HIPCHK(dctq::launch_rle_decode(symbols, offsets, nblocks, coef, (hipStream_t)stream, device_cus()),
+           "rle_decode launch");
+    return DCTQ_OK;
+}
+
 int dctq_device_count(int *count) {
     DCTQ_ENTRY;
     HIPCHK(hipGetDeviceCount(count), "hipGetDeviceCount");

@@ -76,6 +76,26 @@ int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef
 int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks,
                  float *recon, void *stream);
 
+/* Zigzag + run-length symbols of quantized blocks (the reference's
+ * run_length_encode, src/entropy.c:216-256 over block_to_zigzag :158-178, for
+ * every block, blocks concatenated in order).  symbol = (uint16_t)value |
+ * run << 16.  A block has 1 + (nonzeros among its first 63 zigzag elements)
+ * symbols, so the stream is built in two steps:
+ *   dctq_rle_count: offsets[b] = symbols before block b, offsets[nblocks] =
+ *                   total (nblocks + 1 entries); `workspace` is device memory
+ *                   of dctq_rle_workspace_bytes(nblocks) bytes;
+ *   dctq_rle_emit:  symbols[offsets[b] .. offsets[b+1]) for every block
+ *                   (the caller sizes `symbols` from offsets[nblocks], or
+ *                   64 * nblocks for the worst case).
+ * nblocks < 2^26 (offsets are 32-bit). */
+size_t dctq_rle_workspace_bytes(long long nblocks);
+int dctq_rle_count(const int16_t *coef, long long nblocks, uint32_t *offsets, void *workspace, void *stream);
+int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offsets, uint32_t *symbols, void *stream);
+/* The inverse, run_length_decode (src/entropy.c:327-351) + zigzag_to_block
+ * (:183-210) of every block: coef[b][64] from symbols[offsets[b] ..). */
+int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
+                    void *stream);
+
 /* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented
  * by the number of coefficients resolved by the exact fp64 tie path in later
  * dctq_forward_quant calls on this plan (costs one atomic per affected wave). */

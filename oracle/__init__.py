@@ -4,7 +4,7 @@ ctypes wrappers over
 
 * ``liboracle.so``   -- the clean-room C restatement (``dct_oracle.c``) that
   follows the reference's operation order bit for bit, and
-* ``_ref/libref.so`` -- the reference's own ``src/{utils,dct,quantization}.c``
+* ``_ref/libref.so`` -- the reference's own ``src/{utils,dct,quantization,entropy}.c``
   compiled from ``/root/reference`` by ``oracle/Makefile`` (present when it was
   built in the container; it travels to the GPU box with the snapshot).
 
@@ -61,6 +61,11 @@ def _load_orc():
     lib.orc_splitmix.argtypes = [C.c_uint64, C.c_uint64]
     lib.orc_splitmix.restype = C.c_uint64
     lib.orc_synth_plane.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p, C.c_long]
+    lib.orc_zigzag_order.argtypes = [C.c_int, _ip]
+    lib.orc_rle_encode.argtypes = [C.c_int, _ip, _ip, _ip]
+    lib.orc_rle_decode.argtypes = [C.c_int, _ip, _ip, C.c_int, _ip]
+    lib.orc_rle_encode_plane.argtypes = [_i16p, C.c_long, C.c_void_p, C.c_void_p]
+    lib.orc_rle_encode_plane.restype = C.c_long
     return lib
 
 
@@ -99,6 +104,9 @@ def ref():
         lib.ref_adjust.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, _dp]
         lib.ref_copy_to_coefficients.argtypes = [C.c_int, _dp, _ip]
         lib.ref_forward_plane.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _i16p, C.c_int, C.c_int]
+        lib.ref_rle_encode.argtypes = [C.c_int, _ip, _ip, _ip]
+        lib.ref_rle_decode.argtypes = [C.c_int, _ip, _ip, C.c_int, _ip]
+        lib.ref_zigzag.argtypes = [C.c_int, _ip, _ip]
         lib.ref_forward_plane.restype = C.c_long
         _ref = lib
     return _ref
@@ -206,3 +214,42 @@ def synth_plane(seed: int, kind: int, width: int, height: int) -> np.ndarray:
 
 
 KINDS = {"uniform": 0, "smooth": 1, "const": 2, "extreme": 3}
+
+
+# ---- zigzag + run-length symbols (src/entropy.c:158-256,327-351) -----------
+
+def zigzag_order(n: int = 8) -> np.ndarray:
+    """order[k] = natural (row-major) index of the k-th zigzag element."""
+    o = np.zeros(n * n, np.int32)
+    orc().orc_zigzag_order(n, o)
+    return o
+
+
+def rle_encode(coeffs: np.ndarray):
+    """One block (n x n ints) -> (values, runs) exactly as run_length_encode emits them."""
+    c = np.ascontiguousarray(coeffs, np.int32).ravel()
+    n = int(round(len(c) ** 0.5))
+    v = np.zeros(n * n, np.int32)
+    r = np.zeros(n * n, np.int32)
+    cnt = orc().orc_rle_encode(n, c, v, r)
+    return v[:cnt].copy(), r[:cnt].copy()
+
+
+def rle_decode(values, runs, n: int = 8) -> np.ndarray:
+    v = np.ascontiguousarray(values, np.int32)
+    r = np.ascontiguousarray(runs, np.int32)
+    out = np.zeros(n * n, np.int32)
+    orc().orc_rle_decode(n, v, r, len(v), out)
+    return out.reshape(n, n)
+
+
+def rle_encode_plane(coef: np.ndarray):
+    """int16 [nblk, 64] -> (offsets uint32 [nblk+1], symbols uint32 [total]) in the device format:
+    symbol = (uint16)value | run << 16, blocks in order."""
+    c = np.ascontiguousarray(coef, np.int16).reshape(-1, 64)
+    nblk = c.shape[0]
+    off = np.zeros(nblk + 1, np.uint32)
+    total = orc().orc_rle_encode_plane(c, nblk, off.ctypes.data, None)
+    sym = np.zeros(max(total, 1), np.uint32)
+    orc().orc_rle_encode_plane(c, nblk, off.ctypes.data, sym.ctypes.data)
+    return off, sym[:total]

@@ -320,3 +320,73 @@ void orc_synth_plane(uint64_t seed, int kind, int width, int height, uint8_t *px
     for (int y = 0; y < height; ++y)
         for (int x = 0; x < width; ++x) px[(long)y * stride + x] = orc_synth_pixel(seed, kind, width, x, y);
 }
+
+/* ---- zigzag + run-length symbols ------------------------- */
+
+/* src/entropy.c:158-178: order[k] = natural (row-major) index of the k-th
+ * element of the zigzag traversal (anti-diagonals; even sums walk up-right
+ * from the row maximum, odd sums walk down-left from the row minimum). */
+void orc_zigzag_order(int n, int *order) {
+    int k = 0;
+    for (int sum = 0; sum <= 2 * (n - 1); ++sum) {
+        if (sum % 2 == 0) {
+            for (int i = sum < n ? sum : n - 1; i >= 0 && sum - i < n; --i) order[k++] = i * n + (sum - i);
+        } else {
+            for (int i = sum < n ? 0 : sum - n + 1; i < n && sum - i >= 0; ++i) order[k++] = i * n + (sum - i);
+        }
+    }
+}
+
+/* src/entropy.c:216-256: one (value, run) symbol per nonzero zigzag element,
+ * the run counting the zeros before it, and always a symbol for the LAST
+ * element -- whose run also counts itself when it is zero.  Returns the count. */
+int orc_rle_encode(int n, const int *coeffs, int *values, int *runs) {
+    int order[64 * 64];
+    orc_zigzag_order(n, order);
+    int count = 0, zeros = 0, size = n * n;
+    for (int i = 0; i < size; ++i) {
+        int v = coeffs[order[i]];
+        if (v != 0 || i == size - 1) {
+            if (i == size - 1 && v == 0) zeros++;
+            values[count] = v;
+            runs[count] = zeros;
+            count++;
+            zeros = 0;
+        } else {
+            zeros++;
+        }
+    }
+    return count;
+}
+
+/* src/entropy.c:327-351 (run_length_decode): skip `run` zeros, place the value
+ * (dropped when past the end), then undo the zigzag (:183-210). */
+void orc_rle_decode(int n, const int *values, const int *runs, int count, int *coeffs) {
+    int order[64 * 64], zz[64 * 64];
+    int size = n * n, pos = 0;
+    orc_zigzag_order(n, order);
+    for (int i = 0; i < size; ++i) zz[i] = 0;
+    for (int i = 0; i < count; ++i) {
+        pos += runs[i];
+        if (pos < size) zz[pos++] = values[i];
+    }
+    for (int i = 0; i < size; ++i) coeffs[order[i]] = zz[i];
+}
+
+/* Batched form of the device format (include/dct_amd.h, dctq_rle_*):
+ * offsets[b] = symbols before block b (offsets[nblk] = total), symbol =
+ * (uint16)value | run << 16, blocks in order.  Returns the total. */
+long orc_rle_encode_plane(const int16_t *coef, long nblk, uint32_t *offsets, uint32_t *symbols) {
+    long total = 0;
+    int c[64], v[64], r[64];
+    for (long b = 0; b < nblk; ++b) {
+        for (int k = 0; k < 64; ++k) c[k] = coef[b * 64 + k];
+        int cnt = orc_rle_encode(8, c, v, r);
+        if (offsets) offsets[b] = (uint32_t)total;
+        if (symbols)
+            for (int k = 0; k < cnt; ++k) symbols[total + k] = (uint32_t)(uint16_t)(int16_t)v[k] | ((uint32_t)r[k] << 16);
+        total += cnt;
+    }
+    if (offsets) offsets[nblk] = (uint32_t)total;
+    return total;
+}

@@ -23,4 +23,9 @@ uint64_t orc_splitmix(uint64_t seed, uint64_t i);
 uint8_t orc_synth_pixel(uint64_t seed, int kind, int width, int x, int y);
 void orc_synth_plane(uint64_t seed, int kind, int width, int height, uint8_t *px, long stride);
 
+void orc_zigzag_order(int n, int *order);
+int orc_rle_encode(int n, const int *coeffs, int *values, int *runs);
+void orc_rle_decode(int n, const int *values, const int *runs, int count, int *coeffs);
+long orc_rle_encode_plane(const int16_t *coef, long nblk, uint32_t *offsets, uint32_t *symbols);
+
 #endif

@@ -178,3 +178,45 @@ long ref_forward_plane(unsigned char *px, int width, int height, int quality, in
     quant_free(qc);
     return (long)bh * bw;
 }
+
+/* ---- the reference's run-length coder (src/entropy.c), one block -------- */
+#include <entropy.h>
+
+int ref_rle_encode(int n, const int *coeffs, int *values, int *runs) {
+    int **b = alloc_int_array(n, n);
+    for (int i = 0; i < n; ++i) memcpy(b[i], coeffs + i * n, sizeof(int) * n);
+    EntropyContext *e = entropy_init(0);
+    int cnt = run_length_encode(e, b, n);
+    for (int k = 0; k < cnt; ++k) {
+        values[k] = e->symbols[k].value;
+        runs[k] = e->symbols[k].run_length;
+    }
+    entropy_free(e);
+    free_int_array(b, n);
+    return cnt;
+}
+
+void ref_rle_decode(int n, const int *values, const int *runs, int count, int *coeffs) {
+    EntropyContext *e = entropy_init(0);
+    if (count > e->capacity) {
+        e->symbols = (RLESymbol *)realloc(e->symbols, sizeof(RLESymbol) * count);
+        e->capacity = count;
+    }
+    for (int k = 0; k < count; ++k) {
+        e->symbols[k].value = values[k];
+        e->symbols[k].run_length = runs[k];
+    }
+    e->count = count;
+    int **b = alloc_int_array(n, n);
+    run_length_decode(e, b, n);
+    for (int i = 0; i < n; ++i) memcpy(coeffs + i * n, b[i], sizeof(int) * n);
+    free_int_array(b, n);
+    entropy_free(e);
+}
+
+void ref_zigzag(int n, const int *coeffs, int *zz) {
+    int **b = alloc_int_array(n, n);
+    for (int i = 0; i < n; ++i) memcpy(b[i], coeffs + i * n, sizeof(int) * n);
+    block_to_zigzag(b, zz, n);
+    free_int_array(b, n);
+}

@@ -419,3 +419,32 @@ def test_reference_programs_relinked(T, dm, prog):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == want["rc"], r.stderr
     assert r.stdout == want["stdout"]
+
+
+def test_rle_bit_exact_and_round_trip(T, dm):
+    """Zigzag + RLE on the GPU (src/entropy.c:158-256 per block) == the oracle
+    (pinned to the reference's entropy.c by tests/golden/rle.json), and the GPU
+    decode restores every block (run_length_decode, :327-351)."""
+    import json
+    import oracle as O
+    root = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(root, "golden", "rle.json")))
+    golden = np.array([b["coeffs"] for b in g["blocks"].values()], np.int16)
+    rng = np.random.default_rng(11)
+    cases = [golden, np.zeros((5, 64), np.int16), np.full((3, 64), 7, np.int16),
+             (rng.integers(-600, 600, (1000, 64)) * (rng.random((1000, 64)) < 0.15)).astype(np.int16)]
+    px = O.synth_plane(4, O.KINDS["smooth"], 640, 480)
+    cases.append(O.forward_plane(px, 75, 0))          # real quantized planes: ragged tiles (4800 blocks)
+    cases.append(O.forward_plane(O.synth_plane(5, 0, 512, 256), 90, 1))
+    for c in cases:
+        off, sym = dm.rle_encode(T.from_numpy(c).cuda())
+        woff, wsym = O.rle_encode_plane(c)
+        assert np.array_equal(off.cpu().numpy().view(np.uint32), woff)
+        assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym)
+        back = dm.rle_decode(sym, off).cpu().numpy()
+        assert np.array_equal(back, c)
+    for name, b in g["blocks"].items():  # the reference's own symbols, block by block
+        off, sym = dm.rle_encode(T.from_numpy(np.array([b["coeffs"]], np.int16)).cuda())
+        s = sym.cpu().numpy().view(np.uint32)
+        assert ((s & 0xFFFF).astype(np.uint16).view(np.int16).tolist(), (s >> 16).tolist()) == \
+            (b["values"], b["runs"]), name

@@ -134,3 +134,35 @@ def test_reference_programs_golden():
             pytest.skip("oracle/_ref/test_*_cpu not built (needs /root/reference)")
         r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
         assert (r.returncode, r.stdout) == (w["rc"], w["stdout"]), prog
+
+
+def test_rle_oracle_vs_reference_golden():
+    """Zigzag order and run-length symbols (src/entropy.c:158-256,327-351):
+    the oracle reproduces the reference's own outputs (tests/golden/rle.json)."""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rle.json")))
+    for n, zz in g["zigzag"].items():
+        assert O.zigzag_order(int(n)).tolist() == zz, n
+    for name, b in g["blocks"].items():
+        v, r = O.rle_encode(np.array(b["coeffs"]).reshape(8, 8))
+        assert v.tolist() == b["values"] and r.tolist() == b["runs"], name
+        assert O.rle_decode(v, r).ravel().tolist() == b["decoded"] == b["coeffs"], name
+    # the symbol count is 1 + nnz(all but the last zigzag element) -- what the GPU encoder relies on
+    for name, b in g["blocks"].items():
+        zz = np.array(b["coeffs"])[O.zigzag_order(8)]
+        assert len(b["values"]) == 1 + int(np.count_nonzero(zz[:63])), name
+
+
+def test_rle_plane_format():
+    """Batched device format: offsets + packed (uint16 value | run << 16) symbols."""
+    rng = np.random.default_rng(3)
+    coef = (rng.integers(-50, 50, (300, 64)) * (rng.random((300, 64)) < 0.2)).astype(np.int16)
+    off, sym = O.rle_encode_plane(coef)
+    assert off[0] == 0 and off[-1] == len(sym)
+    for b in range(coef.shape[0]):
+        s = sym[off[b]:off[b + 1]]
+        v = (s & 0xFFFF).astype(np.uint16).view(np.int16)
+        r = s >> 16
+        v2, r2 = O.rle_encode(coef[b].reshape(8, 8))
+        assert v.tolist() == v2.tolist() and r.tolist() == r2.tolist()
