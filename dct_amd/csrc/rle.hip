@@ -12,11 +12,11 @@
 // element i, so "nonzero" is a ballot, a symbol's index is mbcnt of that ballot,
 // its run is the distance to the previous set bit, and the symbols of a block
 // are written by consecutive lanes to consecutive addresses.
-//   dctq_rle_count : per-tile (64 blocks per wave) exclusive offsets + tile totals,
-//                    a one-workgroup scan of the tile totals, a fix-up pass.
-//   dctq_rle_emit  : the symbols.
+//   dctq_rle_count : lane-per-block counts, wave-scanned per 64-block tile, a
+//                    one-workgroup scan of the tile totals, a fix-up pass.
+//   dctq_rle_emit  : the symbols (one wave per tile, block by block).
 //   dctq_rle_decode: run_length_decode (:327-351) + zigzag_to_block (:183-210),
-//                    one wave per block through a 64-entry LDS row.
+//                    one wave per tile through a 64-entry LDS row.
 #include "dctq_internal.h"
 
 namespace dctq {
@@ -38,26 +38,44 @@ constexpr int kScanThreads = 1024;
 
 __device__ __forceinline__ uint64_t lane_mask_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
-// ---- count: tile t = blocks [64t, 64t+64), one wave; lane j ends up with the
-// tile-local exclusive offset of block 64t+j.
+// Inclusive wave scan (DPP row shifts + row broadcasts: VALU only, no LDS).
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t e) {
+    e += __builtin_amdgcn_update_dpp(0u, e, 0x111, 0xF, 0xF, false);  // row_shr:1
+    e += __builtin_amdgcn_update_dpp(0u, e, 0x112, 0xF, 0xF, false);  // row_shr:2
+    e += __builtin_amdgcn_update_dpp(0u, e, 0x114, 0xF, 0xF, false);  // row_shr:4
+    e += __builtin_amdgcn_update_dpp(0u, e, 0x118, 0xF, 0xF, false);  // row_shr:8
+    e += __builtin_amdgcn_update_dpp(0u, e, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    e += __builtin_amdgcn_update_dpp(0u, e, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return e;
+}
+
+// Nonzero int16 halves of a dword (0, 1 or 2).
+__device__ __forceinline__ uint32_t nz16(uint32_t w) { return ((w & 0xFFFFu) != 0u) + ((w >> 16) != 0u); }
+
+// ---- count: tile t = blocks [64t, 64t+64), one wave, lane j = block 64t+j:
+// count = 1 + nnz(the block's first 63 zigzag elements) = 1 + nnz(all) - (c[63] != 0),
+// tile-local exclusive offsets by a wave scan, tile total -> tiles[t].
 __global__ __launch_bounds__(kRleThreads) void rle_count_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                 uint32_t *__restrict__ offsets,
                                                                 uint32_t *__restrict__ tiles, long long ntiles) {
     const int lane = threadIdx.x & 63;
     const long long t = (long long)blockIdx.x * kRleWaves + (threadIdx.x >> 6);
     if (t >= ntiles) return;
-    const long long b0 = t * 64;
-    const int nb = nblk - b0 < 64 ? (int)(nblk - b0) : 64;
-    uint32_t run = 0, mine = 0;
-#pragma unroll 8
-    for (int j = 0; j < nb; ++j) {
-        const int16_t v = coef[(b0 + j) * 64 + lane];  // natural order: count is order-free
-        const uint64_t nz = __builtin_amdgcn_ballot_w64(v != 0 && lane != 63);
-        if (lane == j) mine = run;
-        run += 1u + (uint32_t)__builtin_popcountll(nz);
+    const long long b = t * 64 + lane;
+    uint32_t cnt = 0;
+    if (b < nblk) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(coef + b * 64);
+        uint4 q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = src[k];
+        uint32_t nz = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nz += nz16(q[k].x) + nz16(q[k].y) + nz16(q[k].z) + nz16(q[k].w);
+        cnt = 1u + nz - ((q[7].w >> 16) != 0u);
     }
-    if (lane < nb) offsets[b0 + lane] = mine;
-    if (lane == 0) tiles[t] = run;
+    const uint32_t inc = wave_inclusive_scan(cnt);
+    if (b < nblk) offsets[b] = inc - cnt;
+    if (lane == 63) tiles[t] = inc;
 }
 
 // ---- exclusive scan of the tile totals in place (one workgroup), total -> offsets[nblk]
@@ -92,94 +110,115 @@ __global__ __launch_bounds__(kRleThreads) void rle_fixup_kernel(uint32_t *__rest
     if (b < nblk) offsets[b] += tiles[b >> 6];
 }
 
-// ---- emit: one wave per block (grid-stride), 4 blocks in flight per wave
+// ---- emit: one wave per 64-block tile; lane i holds zigzag element i of the
+// current block; the tile's offsets come in with one coalesced load and are
+// read per block with readlane; 8 blocks' gathers are in flight at a time.
+constexpr int kGroup = 8;
+
 __global__ __launch_bounds__(kRleThreads) void rle_emit_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                const uint32_t *__restrict__ offsets,
-                                                               uint32_t *__restrict__ symbols) {
+                                                               uint32_t *__restrict__ symbols, long long ntiles) {
     const int lane = threadIdx.x & 63;
-    const long long w0 = (long long)blockIdx.x * kRleWaves + (threadIdx.x >> 6);
     const long long stride = (long long)gridDim.x * kRleWaves;
     const int nat = kZigzag[lane];
     const uint64_t below = lane_mask_below(lane);
-    constexpr int U = 4;
-    for (long long b = w0; b < nblk; b += U * stride) {
-        int16_t v[U];
-        uint32_t off[U];
+    for (long long t = (long long)blockIdx.x * kRleWaves + (threadIdx.x >> 6); t < ntiles; t += stride) {
+        const long long b0 = t * 64;
+        const int nb = nblk - b0 < 64 ? (int)(nblk - b0) : 64;
+        const uint32_t offv = lane < nb ? offsets[b0 + lane] : 0u;
+        for (int g = 0; g < nb; g += kGroup) {
+            int16_t v[kGroup];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const long long bb = b + u * stride < nblk ? b + u * stride : b;
-            v[u] = coef[bb * 64 + nat];
-            off[u] = offsets[bb];
-        }
+            for (int u = 0; u < kGroup; ++u) v[u] = coef[(b0 + (g + u < nb ? g + u : g)) * 64 + nat];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (b + u * stride >= nblk) break;
-            const bool emit = v[u] != 0 || lane == 63;
-            const uint64_t m = __builtin_amdgcn_ballot_w64(emit);
-            const uint64_t prev = m & below;
-            const int p = prev ? 63 - __builtin_clzll(prev) : -1;
-            const uint32_t runlen = (uint32_t)(lane - p - 1) + (lane == 63 && v[u] == 0 ? 1u : 0u);
-            const uint32_t idx = (uint32_t)__builtin_popcountll(prev);
-            if (emit) symbols[off[u] + idx] = (uint32_t)(uint16_t)v[u] | (runlen << 16);
+            for (int u = 0; u < kGroup; ++u) {
+                if (g + u >= nb) break;
+                const uint32_t o = __builtin_amdgcn_readlane(offv, g + u);
+                const bool emit = v[u] != 0 || lane == 63;
+                const uint64_t prev = __builtin_amdgcn_ballot_w64(emit) & below;
+                const int p = prev ? 63 - __builtin_clzll(prev) : -1;
+                const uint32_t runlen = (uint32_t)(lane - p - 1) + (lane == 63 && v[u] == 0 ? 1u : 0u);
+                if (emit) symbols[o + (uint32_t)__builtin_popcountll(prev)] = (uint32_t)(uint16_t)v[u] | (runlen << 16);
+            }
         }
     }
 }
 
-// ---- decode: one wave per block; the block is rebuilt in a 64-entry LDS row
-// (zeroed, symbols scattered to their zigzag positions in program order), then
-// read back in natural order and stored as 128 contiguous bytes.
+// ---- decode: one wave per 64-block tile, groups of 8 blocks: the symbol loads
+// of a group are in flight together (each block's range from readlane of the
+// tile's coalesced offsets); each block is rebuilt in the wave's 64-entry LDS
+// row (zeroed, symbols scattered to their zigzag positions -- LDS writes of one
+// wave are performed in order), read back in natural order, and the group's 8
+// blocks are stored as 128-B rows.
 //
 // LDS loads and the store-data race (fdct8.hip v2 / DESIGN.md): the previous
-// block's store may still be reading its data VGPR when this block's LDS read
-// returns.  That VGPR (`outv`) is kept live across the read, so the LDS read
-// can never land in it; the store's address operands are loop-invariant.
+// group's stores may still be reading their data VGPRs when this group's LDS
+// reads return, so those 8 registers are kept live across the reads (the LDS
+// reads cannot land in them); the stores' address operands are loop-invariant
+// (voff) or scalar.
 __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t *__restrict__ symbols,
                                                                  const uint32_t *__restrict__ offsets, long long nblk,
-                                                                 int16_t *__restrict__ coef) {
+                                                                 int16_t *__restrict__ coef, long long ntiles) {
     __shared__ int16_t row[kRleWaves][64];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long w0 = (long long)blockIdx.x * kRleWaves + wv;
     const long long stride = (long long)gridDim.x * kRleWaves;
     const int zpos = kUnzigzag[lane];
-    uint32_t outv = 0, voff = (uint32_t)lane * 2u;  // voff: loop-invariant and live, see above
-    for (long long b = w0; b < nblk; b += stride) {
-        const uint32_t o0 = offsets[b], o1 = offsets[b + 1];
-        const uint32_t cnt = o1 - o0;
-        const uint32_t s = lane < (int)cnt ? symbols[o0 + lane] : 0u;
-        // end position of symbol k = sum_{j<=k} (run_j + 1): inclusive wave scan (DPP, VALU only)
-        uint32_t e = lane < (int)cnt ? (s >> 16) + 1u : 0u;
-        e += __builtin_amdgcn_update_dpp(0u, e, 0x111, 0xF, 0xF, false);  // row_shr:1
-        e += __builtin_amdgcn_update_dpp(0u, e, 0x112, 0xF, 0xF, false);  // row_shr:2
-        e += __builtin_amdgcn_update_dpp(0u, e, 0x114, 0xF, 0xF, false);  // row_shr:4
-        e += __builtin_amdgcn_update_dpp(0u, e, 0x118, 0xF, 0xF, false);  // row_shr:8
-        e += __builtin_amdgcn_update_dpp(0u, e, 0x142, 0xA, 0xF, false);  // row_bcast:15
-        e += __builtin_amdgcn_update_dpp(0u, e, 0x143, 0xC, 0xF, false);  // row_bcast:31
-        row[wv][lane] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t pos = e - 1u;  // run_length_decode: pos += run; zigzag[pos++] = value (dropped past the end)
-        if (lane < (int)cnt && pos < 64u) row[wv][pos] = (int16_t)(s & 0xFFFFu);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        asm volatile("" : "+v"(outv));  // previous block's store data stays live across the LDS read
-        const int16_t val = row[wv][zpos];
-        asm volatile("" ::"v"(outv));
-        outv = (uint32_t)(uint16_t)val;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(coef + b * 64, (short)0, 128, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)outv, rs, voff, 0, 0);
-        asm volatile("" : "+v"(voff));
+    uint32_t voff = (uint32_t)lane * 2u;
+    uint32_t outv[kGroup];
+#pragma unroll
+    for (int u = 0; u < kGroup; ++u) outv[u] = 0;
+    for (long long t = (long long)blockIdx.x * kRleWaves + wv; t < ntiles; t += stride) {
+        const long long b0 = t * 64;
+        const int nb = nblk - b0 < 64 ? (int)(nblk - b0) : 64;
+        const uint32_t offv = offsets[b0 + (lane < nb ? lane : nb)];  // lane nb: the end of the tile
+        for (int g = 0; g < nb; g += kGroup) {
+            uint32_t sy[kGroup], cnt[kGroup];
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                const int jb = g + u < nb ? g + u : nb - 1;
+                const uint32_t o0 = __builtin_amdgcn_readlane(offv, jb), o1 = __builtin_amdgcn_readlane(offv, jb + 1);
+                cnt[u] = g + u < nb ? o1 - o0 : 0u;
+                sy[u] = (uint32_t)lane < cnt[u] ? symbols[o0 + lane] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) asm volatile("" : "+v"(outv[u]));
+            uint32_t val[kGroup];
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                const uint32_t e = wave_inclusive_scan((uint32_t)lane < cnt[u] ? (sy[u] >> 16) + 1u : 0u);
+                row[wv][lane] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t pos = e - 1u;  // run_length_decode: pos += run; zigzag[pos++] = value (dropped past the end)
+                if ((uint32_t)lane < cnt[u] && pos < 64u) row[wv][pos] = (int16_t)(sy[u] & 0xFFFFu);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                val[u] = (uint32_t)(uint16_t)row[wv][zpos];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) asm volatile("" ::"v"(outv[u]));
+#pragma unroll
+            for (int u = 0; u < kGroup; ++u) {
+                outv[u] = val[u];
+                if (g + u < nb) {
+                    const __amdgpu_buffer_rsrc_t rs =
+                        __builtin_amdgcn_make_buffer_rsrc(coef + (b0 + g + u) * 64, (short)0, 128, 0x00020000);
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)outv[u], rs, voff, 0, 0);
+                }
+            }
+            asm volatile("" : "+v"(voff));
+        }
     }
 }
 
 static unsigned grid_for(long long waves_wanted, int num_cus) {
     long long g = (waves_wanted + kRleWaves - 1) / kRleWaves;
-    const long long cap = (long long)num_cus * 8;
+    const long long cap = (long long)num_cus * 16;
     return (unsigned)(g < 1 ? 1 : g > cap ? cap : g);
 }
 
@@ -198,15 +237,17 @@ hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offse
 
 hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,
                            hipStream_t stream, int num_cus) {
-    hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(nblk, num_cus)), dim3(kRleThreads), 0, stream, coef, nblk,
-                       offsets, symbols);
+    const long long ntiles = (nblk + 63) / 64;
+    hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, coef, nblk,
+                       offsets, symbols, ntiles);
     return hipGetLastError();
 }
 
 hipError_t launch_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblk, int16_t *coef,
                              hipStream_t stream, int num_cus) {
-    hipLaunchKernelGGL(rle_decode_kernel, dim3(grid_for(nblk, num_cus)), dim3(kRleThreads), 0, stream, symbols,
-                       offsets, nblk, coef);
+    const long long ntiles = (nblk + 63) / 64;
+    hipLaunchKernelGGL(rle_decode_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, symbols,
+                       offsets, nblk, coef, ntiles);
     return hipGetLastError();
 }
 

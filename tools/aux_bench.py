@@ -39,3 +39,41 @@ for var, ad in [(v, a) for a in (0, 1) for v in ("1", "2")]:
         med = statistics.median(ts)
         print(f"{name:27s} median {med*1e6:8.1f} us  {nblk/med/1e9:6.2f} Gblk/s  {nblk*bpb/med/1e9:6.0f} GB/s "
               f"({nblk*bpb/med/8e12*100:5.1f}% of 8 TB/s, {bpb} B/block)")
+
+
+# ---- zigzag + RLE on the forward-quant output (q50): count+emit and decode
+for kind in ("uniform", "smooth"):
+    os.environ["DCTQ_FDCT_VARIANT"] = "2"
+    px2 = dct_amd.synth(9, kind, W, H, F)
+    plan = dct_amd.Plan(50, 0)
+    coef = plan.forward_quant(px2)
+    off, sym = dct_amd.rle_encode(coef)
+    total = sym.numel()
+    back = torch.empty_like(coef)
+    ws = torch.empty(int(dct_amd.lib().dctq_rle_workspace_bytes(nblk)) // 4 + 1, dtype=torch.int32, device="cuda")
+    L = dct_amd.lib()
+    import ctypes as C
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    jobs = {
+        "rle_count": (lambda: L.dctq_rle_count(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(off.data_ptr()),
+                                               C.c_void_p(ws.data_ptr()), s), nblk * (128 + 4 + 8)),
+        "rle_emit": (lambda: L.dctq_rle_emit(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(off.data_ptr()),
+                                             C.c_void_p(sym.data_ptr()), s), nblk * (128 + 4) + 4 * total),
+        "rle_decode": (lambda: L.dctq_rle_decode(C.c_void_p(sym.data_ptr()), C.c_void_p(off.data_ptr()), nblk,
+                                                 C.c_void_p(back.data_ptr()), s), nblk * (128 + 4) + 4 * total),
+    }
+    for name, (fn, nbytes) in jobs.items():
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(8):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e-3)
+        med = statistics.median(ts)
+        print(f"{name + ' ' + kind:27s} median {med*1e6:8.1f} us  {nblk/med/1e9:6.2f} Gblk/s  {nbytes/med/1e9:6.0f} GB/s "
+              f"({nbytes/med/8e12*100:5.1f}% of 8 TB/s, {nbytes/nblk:.0f} B/block, {total/nblk:.1f} symbols/block)")
+    assert torch.equal(back, coef)
