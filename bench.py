@@ -11,8 +11,10 @@ in HBM; one step = dctq_forward_quant over every block of the batch (two
 launches: the F luma planes, then the 2F chroma planes), int16 coefficients
 bit-exact with the reference.  N>1: one process per GPU (torch.distributed),
 each rank its own F frames (weak scaling, no data-path collective); value =
-all blocks / max-over-ranks wall time.  At N>1 a second, separately reported
-leg ("gather") times forward DCT+quant of the luma frames followed by the RCCL
+all blocks / max-over-ranks wall time.  A separately reported leg
+("round_trip", BASELINE configs[4]) runs forward DCT+quant then dequant+IDCT
+over the same frames and reports end-to-end blocks/s and PSNR.  At N>1 a
+second, separately reported leg ("gather") times forward DCT+quant of the luma frames followed by the RCCL
 all-gather of every rank's int16 coefficient planes (BASELINE configs[3],
 SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange.
 
@@ -55,6 +57,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
+    ap.add_argument("--round-trip-steps", type=int, default=3,
+                    help="timed steps of the config-5 round trip leg (forward+inverse, PSNR); 0 = skip")
     ap.add_argument("--backend", default="nccl", help="N>1 process group (nccl = RCCL; gloo only to rehearse "
                                                       "several ranks on one GPU)")
     return ap.parse_args()
@@ -119,6 +123,57 @@ def gather_leg(args, plan, luma, coef_y, world, rank, dev):
             "blocks_per_s": world * n * args.gather_steps / el, "ms_per_step": el / args.gather_steps * 1e3,
             "bytes_received_per_rank": (world - 1) * n * 128, "steps": args.gather_steps,
             "own_slice_intact": ok}
+
+
+def round_trip_leg(args, plan, luma, chroma, world, dev):
+    """BASELINE configs[4]: forward DCT+quant then dequant+IDCT of every plane of
+    the frame stream (unfused: dctq_forward_quant with var_num, dctq_inverse),
+    end-to-end blocks/s (max over ranks) and PSNR of the first luma frame vs its
+    input, with the reference's formula (recon clamped to [0,255],
+    tests/test_entropy.c:376-393).  Non-adaptive plans reproduce the reference's
+    1/Q dequantization (src/quantization.c:139,144), hence their low PSNR."""
+    planes = []
+    for px in (luma, chroma):
+        f, h, w = px.shape
+        n = f * (h // 8) * (w // 8)
+        planes.append((px, torch.empty((n, 64), dtype=torch.int16, device=dev),
+                       torch.empty(n, dtype=torch.int32, device=dev),
+                       torch.empty((n, 64), dtype=torch.float32, device=dev)))
+
+    def once():
+        for px, co, vn, rec in planes:
+            plan.forward_quant(px, out=co, var_num=vn)
+            plan.inverse(co, var_num=vn, out=rec)
+
+    once()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.round_trip_steps):
+        once()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    nblk = sum(p[1].shape[0] for p in planes)
+    # PSNR of luma frame 0 (block order is raster, so compare block by block)
+    px, _, _, rec = planes[0]
+    h, w = px.shape[1], px.shape[2]
+    n0 = (h // 8) * (w // 8)
+    orig = px[0].reshape(h // 8, 8, w // 8, 8).permute(0, 2, 1, 3).reshape(n0, 64).double()
+    mse = float(((orig - rec[:n0].double().clamp(0, 255)) ** 2).mean())
+    psnr = float("inf") if mse == 0 else 10.0 * __import__("math").log10(255.0 * 255.0 / mse)
+    bpb = 64 + 128 + 4 + 128 + 4 + 256
+    return {"op": "forward_quant(var_num) + inverse over all planes (unfused)", "steps": args.round_trip_steps,
+            "blocks_per_s": world * nblk * args.round_trip_steps / el,
+            "ms_per_step": el / args.round_trip_steps * 1e3,
+            "bytes_per_block": bpb, "achieved_GBs_per_gpu": nblk * bpb * args.round_trip_steps / el / 1e9,
+            "psnr_db_luma_frame0": psnr,
+            "psnr_note": "bug-compatible 1/Q dequantization for adaptive=0 (reference semantics)"}
 
 
 def main():
@@ -202,6 +257,10 @@ def main():
     if world > 1 and args.gather_steps > 0:
         gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
 
+    round_trip = None
+    if args.round_trip_steps > 0:
+        round_trip = round_trip_leg(args, plan, luma, chroma, world, dev)
+
     total_blocks = world * (nblk_y + nblk_c) * args.steps
     value = total_blocks / el
     traffic = None
@@ -239,6 +298,7 @@ def main():
             "cpu_baseline": cpu,
             "parity_check": parity,
             "gather": gather,
+            "round_trip": round_trip,
             "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
                     "reference-order recomputation for guard-band (tie) coefficients",
         }
