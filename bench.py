@@ -7,9 +7,9 @@
 Metric (BASELINE.json): 8x8 macroblocks/s (DCT+quant) and % of HBM roofline.
 Workload: a stream of 4K 4:2:0 frames (BASELINE configs[2] planes: Y 3840x2160 +
 Cb/Cr 1920x1080 = 194,400 blocks per frame), F frames per GPU per step, resident
-in HBM; one step = dctq_forward_quant over every block of the batch (two
-launches: the F luma planes, then the 2F chroma planes), int16 coefficients
-bit-exact with the reference.  N>1: one process per GPU (torch.distributed),
+in HBM; one step = dctq_forward_quant_planes over every block of the batch (ONE
+launch: plane 0 = the F luma frames, plane 1 = the 2F chroma frames; --per-plane
+times the two-launch form), int16 coefficients bit-exact with the reference.  N>1: one process per GPU (torch.distributed),
 each rank its own F frames (weak scaling, no data-path collective); value =
 all blocks / max-over-ranks wall time.  A separately reported leg
 ("round_trip", BASELINE configs[4]) runs forward DCT+quant then dequant+IDCT
@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
     ap.add_argument("--round-trip-steps", type=int, default=3,
                     help="timed steps of the config-5 round trip leg (forward+inverse, PSNR); 0 = skip")
+    ap.add_argument("--per-plane", action="store_true",
+                    help="two launches per step (luma, then chroma) instead of one multi-plane launch")
     ap.add_argument("--backend", default="nccl", help="N>1 process group (nccl = RCCL; gloo only to rehearse "
                                                       "several ranks on one GPU)")
     return ap.parse_args()
@@ -141,8 +143,9 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
                        torch.empty((n, 64), dtype=torch.float32, device=dev)))
 
     def once():
+        plan.forward_quant_planes([p[0] for p in planes], outs=[p[1] for p in planes],
+                                  var_nums=[p[2] for p in planes])
         for px, co, vn, rec in planes:
-            plan.forward_quant(px, out=co, var_num=vn)
             plan.inverse(co, var_num=vn, out=rec)
 
     once()
@@ -168,7 +171,7 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
     mse = float(((orig - rec[:n0].double().clamp(0, 255)) ** 2).mean())
     psnr = float("inf") if mse == 0 else 10.0 * __import__("math").log10(255.0 * 255.0 / mse)
     bpb = 64 + 128 + 4 + 128 + 4 + 256
-    return {"op": "forward_quant(var_num) + inverse over all planes (unfused)", "steps": args.round_trip_steps,
+    return {"op": "forward_quant_planes(var_num) + inverse per plane (unfused)", "steps": args.round_trip_steps,
             "blocks_per_s": world * nblk * args.round_trip_steps / el,
             "ms_per_step": el / args.round_trip_steps * 1e3,
             "bytes_per_block": bpb, "achieved_GBs_per_gpu": nblk * bpb * args.round_trip_steps / el / 1e9,
@@ -203,13 +206,18 @@ def main():
     plan = dct_amd.Plan(args.quality, args.adaptive)
     torch.cuda.synchronize()
 
+    launches = 2 if args.per_plane else 1
+
     def step(ev=None):
         if ev is not None:
             ev[0].record()
-        plan.forward_quant(luma, out=coef_y)
-        if ev is not None:
-            ev[1].record()
-        plan.forward_quant(chroma, out=coef_c)
+        if args.per_plane:
+            plan.forward_quant(luma, out=coef_y)
+            if ev is not None:
+                ev[1].record()
+            plan.forward_quant(chroma, out=coef_c)
+        else:
+            plan.forward_quant_planes([luma, chroma], outs=[coef_y, coef_c])
         if ev is not None:
             ev[2].record()
 
@@ -232,12 +240,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    # per-launch kernel durations (HIP events on the launch stream)
-    ky = [e[0].elapsed_time(e[1]) * 1e-3 for e in evs]
-    kc = [e[1].elapsed_time(e[2]) * 1e-3 for e in evs]
-    launches = 2 * args.steps
-    avg_launch_s = (sum(ky) + sum(kc)) / launches
-    avg_launch_bytes = BYTES_PER_BLOCK * (nblk_y + nblk_c) / 2
+    # per-launch kernel durations (HIP events on the launch stream; the events
+    # bracket the launches only, so in the two-launch form they include the gap)
+    kt = [e[0].elapsed_time(e[2]) * 1e-3 for e in evs]
+    avg_launch_s = sum(kt) / (launches * args.steps)
+    avg_launch_bytes = BYTES_PER_BLOCK * (nblk_y + nblk_c) / launches
     achieved = avg_launch_bytes / avg_launch_s / 1e9
 
     # quick parity self-check of the last step: one chroma plane vs the oracle
@@ -267,7 +274,8 @@ def main():
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("frames") == F and tj.get("kind") == args.kind:
+            if (tj.get("frames") == F and tj.get("kind") == args.kind
+                    and tj.get("launches_per_step", 2) == launches):
                 traffic = tj.get("bytes_per_launch")
         except Exception:
             traffic = None
@@ -293,7 +301,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"fdct8_quant_v2<{bool(args.adaptive)}, false, false>".lower(),
-                         "avg_launch_us": avg_launch_s * 1e6,
+                         "avg_launch_us": avg_launch_s * 1e6, "launches_per_step": launches,
                          "bytes_per_launch": avg_launch_bytes},
             "cpu_baseline": cpu,
             "parity_check": parity,

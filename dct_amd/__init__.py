@@ -46,6 +46,7 @@ def lib() -> C.CDLL:
             "dctq_plan_destroy": ([vp], None),
             "dctq_plan_set_fallback_counter": ([vp, vp], i),
             "dctq_forward_quant": ([vp, C.POINTER(_Plane), vp, vp, vp], i),
+            "dctq_forward_quant_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
             "dctq_inverse": ([vp, vp, vp, ll, vp, vp], i),
             "dctq_synth": ([C.c_uint64, i, C.POINTER(_Plane), vp], i),
@@ -129,6 +130,22 @@ class Plan:
                                         C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
                                         _stream_ptr(stream)))
         return out
+
+    def forward_quant_planes(self, planes, outs=None, var_nums=None, stream=None):
+        """Up to 4 u8 planes of any geometry (e.g. Y, Cb, Cr) in ONE launch; returns the list
+        of int16 [nblk_k, 64] outputs, each equal to forward_quant(planes[k])."""
+        import torch
+        n = len(planes)
+        descs = (_Plane * n)(*[plane_desc(px) for px in planes])
+        if outs is None:
+            outs = [torch.empty((d.nframes * (d.width // 8) * (d.height // 8), 64), dtype=torch.int16,
+                                device=px.device) for d, px in zip(descs, planes)]
+        cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+        vp = (C.c_void_p * n)(*[v.data_ptr() for v in var_nums]) if var_nums is not None else None
+        _check(lib().dctq_forward_quant_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
+                                               C.cast(vp, C.c_void_p) if vp is not None else None,
+                                               _stream_ptr(stream)))
+        return outs
 
     def forward_float(self, px, out=None, stream=None):
         import torch

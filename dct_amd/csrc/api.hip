@@ -240,18 +240,37 @@ int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter)
     return DCTQ_OK;
 }
 
-int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num, void *stream) {
+int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                              int32_t *const *var_num, void *stream) {
     DCTQ_ENTRY;
-    if (!plan || !coef) return fail(DCTQ_EINVAL, "plan/coef is NULL");
-    if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
-    dctq::PlaneArgs a;
-    int rc = plane_args(src, &a);
-    if (rc) return rc;
-    HIPCHK(dctq::launch_fdct8_quant(a, plan->fast, plan->dev, plan->adaptive, coef, var_num, plan->fallbacks,
-                                    (hipStream_t)stream, plan->variant, plan->num_cus, plan->ring,
-                                    plan->ring_wgs),
+    if (!plan || !planes || !coef) return fail(DCTQ_EINVAL, "plan/planes/coef is NULL");
+    if (nplanes < 1 || nplanes > dctq::kMaxPlanes) return fail(DCTQ_EINVAL, "nplanes must be in [1, 4]");
+    dctq::PlaneSet ps = {};
+    ps.n = nplanes;
+    uint32_t first = 0;
+    for (int k = 0; k < nplanes; ++k) {
+        if (!coef[k]) return fail(DCTQ_EINVAL, "coef[k] is NULL");
+        if (((uintptr_t)coef[k]) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
+        if (var_num && !var_num[k]) return fail(DCTQ_EINVAL, "var_num given but var_num[k] is NULL");
+        int rc = plane_args(&planes[k], &ps.pl[k]);
+        if (rc) return rc;
+        ps.coef[k] = coef[k];
+        ps.var[k] = var_num ? var_num[k] : nullptr;
+        ps.first[k] = first;
+        first += (uint32_t)((ps.pl[k].nblk + 63) / 64);  // < 4 * 2^25
+    }
+    ps.first[nplanes] = first;
+    for (int k = nplanes + 1; k <= dctq::kMaxPlanes; ++k) ps.first[k] = first;
+    HIPCHK(dctq::launch_fdct8_quant(ps, plan->fast, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
+                                    plan->variant, plan->num_cus, plan->ring, plan->ring_wgs),
            "fdct8_quant launch");
     return DCTQ_OK;
+}
+
+int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num, void *stream) {
+    DCTQ_ENTRY;
+    if (!src) return fail(DCTQ_EINVAL, "plane is NULL");
+    return dctq_forward_quant_planes(plan, src, 1, &coef, var_num ? &var_num : nullptr, stream);
 }
 
 int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream) {

@@ -68,9 +68,19 @@ struct PlaneArgs {
     FastDiv div_bw, div_frame;  // by bw and by nblk_frame
 };
 
-hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
-                              int16_t *coef, int32_t *var_num, unsigned long long *fallbacks,
-                              hipStream_t stream, int variant, int num_cus, void *ring, int ring_wgs);
+// Up to kMaxPlanes planes (e.g. Y, Cb, Cr) processed by ONE forward launch.
+constexpr int kMaxPlanes = 4;
+struct PlaneSet {
+    PlaneArgs pl[kMaxPlanes];
+    int16_t *coef[kMaxPlanes];
+    int32_t *var[kMaxPlanes];          // all NULL or all set
+    uint32_t first[kMaxPlanes + 1];    // global index of each plane's first 64-block batch; first[n] = total
+    int n;
+};
+
+hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
+                              unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus, void *ring,
+                              int ring_wgs);
 // bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
 size_t fdct8_ring_bytes(int workgroups);
 hipError_t launch_fdct8_float_pair(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream,

@@ -281,7 +281,7 @@ constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) con
 #define DCTQ_LOAD_NT 1  // pixel rows are read exactly once
 #endif
 #ifndef DCTQ_ABLATE
-#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores
+#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores
 #endif
 
 template <int K>
@@ -369,20 +369,37 @@ __device__ int exact_entry(const uint4 *__restrict__ stash, int c, const DevTabl
     return (int)round(out / m);
 }
 
+// Coefficient output of plane k (k wave-uniform or not: a select chain, no indexed kernarg loads).
+__device__ __forceinline__ int16_t *coef_of(const PlaneSet &ps, uint32_t k) {
+    int16_t *c = ps.coef[0];
+#pragma unroll
+    for (int i = 1; i < kMaxPlanes; ++i) c = k == (uint32_t)i ? ps.coef[i] : c;
+    return c;
+}
+
+// Plane of global batch g (wave-uniform).
+__device__ __forceinline__ int plane_of(const PlaneSet &ps, uint32_t g) {
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxPlanes; ++i) k += (i < ps.n && g >= ps.first[i]) ? 1 : 0;
+    return k;
+}
+
+// Exact recomputation of up to 64 queued (block, coefficient) entries, one per
+// lane, patched into their planes' coefficient arrays.
 template <bool ADAPTIVE, bool STATS>
-__device__ __forceinline__ void drain_queue(const DevTables *__restrict__ dev, int16_t *__restrict__ coef,
-                                            const uint32_t *q, const uint4 *ring, int &qn, int lane,
+__device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables *__restrict__ dev, const uint32_t *qb,
+                                            const uint16_t *qc, const uint4 *ring, int &qn, int lane,
                                             unsigned long long *fallbacks) {
     // the wave's own coefficient stores (and its stash stores) must land first
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     const int take = qn < 64 ? qn : 64;
     if (lane < take) {
         const int slot = qn - take + lane;
-        const uint32_t e = q[slot];
-        const uint32_t n = e >> 6;
+        const uint32_t n = qb[slot], e = qc[slot];
         const int c = (int)(e & 63u);
         const int val = exact_entry<ADAPTIVE>(ring + slot * 4, c, dev);
-        coef[(size_t)n * 64 + c] = (int16_t)val;
+        coef_of(ps, e >> 6)[(size_t)n * 64 + c] = (int16_t)val;
     }
     qn -= take;
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
@@ -459,7 +476,7 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
         for (int i = 0; i < 8; ++i) {
             const int c = i * 8 + c0, slot = 16 * cp + 2 * i;
             const f2 y = {v[i][c0], v[i][c0 + 1]};
-            f2 w = {tp->ws[slot], tp->ws[slot + 1]};
+            f2 w = (DCTQ_ABLATE & 256) ? f2{0.0625f + slot * 1e-3f, 0.0625f} : f2{tp->ws[slot], tp->ws[slot + 1]};
             if (ADAPTIVE) {
                 if (c == 0) w.y *= sc2.y;  // the DC keeps Q (src/quantization.c:198-199)
                 else w *= sc2;
@@ -467,7 +484,7 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
             const f2 tt = __builtin_elementwise_fma(y, w, M2);
             const f2 nr = M2 - tt;
             const f2 f = __builtin_elementwise_fma(y, w, nr);
-            const f2 T = {tp->t2s[slot], tp->t2s[slot + 1]};
+            const f2 T = (DCTQ_ABLATE & 256) ? f2{0.25f, 0.25f} : f2{tp->t2s[slot], tp->t2s[slot + 1]};
             const f2 d = __builtin_elementwise_fma(-f, f, T);  // < 0  <=>  |f| beyond the guard
             if (DCTQ_ABLATE & 1) {
             } else if (cp < 2) {
@@ -489,16 +506,26 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
 // One 64-block batch of the v2 loop.  `nxt` holds this batch's rows on entry and
 // the next batch's rows on exit.
 template <bool ADAPTIVE, bool VAR, bool STATS>
-__device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables *__restrict__ dev,
-                                            int16_t *__restrict__ coef, int32_t *__restrict__ var_out,
-                                            unsigned long long *fallbacks, uint4 *stage, uint32_t *q, uint4 *ring,
-                                            int &qn, uint2 (&nxt)[8], uint32_t b, uint32_t step, int lane, int wv) {
+__device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables *__restrict__ dev,
+                                            unsigned long long *fallbacks, uint4 *stage, uint32_t *qb, uint16_t *qc,
+                                            uint4 *ring, int &qn, uint2 (&nxt)[8], uint32_t g, uint32_t step, int lane,
+                                            int wv) {
+    // global batch g -> plane k, plane-local batch b (wave-uniform)
+    const int k = plane_of(ps, g);
+    const PlaneArgs &p = ps.pl[k];
+    const uint32_t b = g - ps.first[k];
+    int16_t *__restrict__ coef = ps.coef[k];
+    int32_t *__restrict__ var_out = ps.var[k];
     uint2 cur[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
     const uint32_t n = b * 64 + lane;
     const bool valid = n < (uint32_t)p.nblk;
-    load_rows(p, (b + step) * 64 + lane, nxt);  // unconditional: past the end it re-reads block 0
+    {
+        const uint32_t gn = g + step;  // past the end: the last plane's block 0 (re-read, unused)
+        const int kn = plane_of(ps, gn);
+        load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
+    }
 
     uint32_t mlo, mhi;
     int32_t var_num;
@@ -512,7 +539,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
         const uint32_t w = cur[0].x;
         bool flat = w == (w & 0xFFu) * 0x01010101u;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) flat = flat && cur[r].x == w && cur[r].y == w;
+        for (int r = 0; r < 8; ++r) flat &= (cur[r].x == w) & (cur[r].y == w);  // bitwise: no short-circuit branches
         if ((mlo >> 31) && flat) {
             reinterpret_cast<int16_t *>(stage)[(wv * 64 + lane) * (kPitch2 / 2)] = dev->dc_const[w & 0xFFu];
             mlo &= 0x7FFFFFFFu;
@@ -573,7 +600,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
     while (has) {
         if (qn > kQCap - 64) {
             if (DCTQ_ABLATE & 16) qn = 0;
-            else drain_queue<ADAPTIVE, STATS>(dev, coef, q, ring, qn, lane, fallbacks);
+            else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
         }
         if (mlo | mhi) {
             int slot;
@@ -581,57 +608,63 @@ __device__ __forceinline__ void fdct8_batch(const PlaneArgs &p, const DevTables 
                 slot = __clz(mlo);
                 mlo &= ~(0x80000000u >> slot);
             } else {
-                const int k = __clz(mhi);
-                mhi &= ~(0x80000000u >> k);
-                slot = 32 + k;
+                const int z = __clz(mhi);
+                mhi &= ~(0x80000000u >> z);
+                slot = 32 + z;
             }
             // slot = 16*cp + 2*i + h  ->  coefficient 8*i + 2*cp + h
             const int c = (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
             const uint32_t pos =
                 qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
-            q[pos] = (n << 6) | (uint32_t)c;
+            qb[pos] = n;
+            qc[pos] = (uint16_t)((uint32_t)c | ((uint32_t)k << 6));
             // stash the block's pixels while they are still in registers: the
             // drain must not go back to HBM for them (8 random 64-B bursts per entry)
             uint4 *st = ring + pos * 4;
+            if (!(DCTQ_ABLATE & 1024))
 #pragma unroll
-            for (int k = 0; k < 4; ++k) st[k] = make_uint4(cur[2 * k].x, cur[2 * k].y, cur[2 * k + 1].x, cur[2 * k + 1].y);
+                for (int k = 0; k < 4; ++k)
+                    st[k] = make_uint4(cur[2 * k].x, cur[2 * k].y, cur[2 * k + 1].x, cur[2 * k + 1].y);
         }
         qn += __builtin_popcountll(has);
         has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
     }
     if (qn >= 64) {
         if (DCTQ_ABLATE & 16) qn = 0;
-        else drain_queue<ADAPTIVE, STATS>(dev, coef, q, ring, qn, lane, fallbacks);
+        else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
     }
 }
 
 template <bool ADAPTIVE, bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneArgs p, FastTables t,
+__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneSet ps, FastTables t,
                                                               const DevTables *__restrict__ dev,
-                                                              int16_t *__restrict__ coef,
-                                                              int32_t *__restrict__ var_out,
                                                               unsigned long long *fallbacks, uint4 *ring_all) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ uint32_t queue[kWaves * kQCap];
+    __shared__ uint32_t qblk[kWaves * kQCap];
+    __shared__ uint16_t qcoef[kWaves * kQCap];
     // readfirstlane: the wave index is uniform, so batch pointers and buffer
     // descriptors live in SGPRs (no waterfall loops around the stores)
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nbatch = ((uint32_t)p.nblk + 63u) >> 6;
+    const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kWaves;
-    uint32_t *q = queue + wv * kQCap;
+    uint32_t *qb = qblk + wv * kQCap;
+    uint16_t *qc = qcoef + wv * kQCap;
     uint4 *ring = ring_all + (size_t)(blockIdx.x * kWaves + wv) * kQCap * 4;  // 64 B per queue slot
     int qn = 0;
-    uint32_t b = blockIdx.x * kWaves + wv;
+    uint32_t g = blockIdx.x * kWaves + wv;
     uint2 nxt[8];
-    load_rows(p, b * 64 + lane, nxt);
+    {
+        const int k0 = plane_of(ps, g);
+        load_rows(ps.pl[k0], (g - ps.first[k0]) * 64 + lane, nxt);
+    }
     // same fence as at the end of a batch: the loop header then sees no load in
     // flight on either incoming edge and needs no wait at all
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-    for (; b < nbatch; b += step)
-        fdct8_batch<ADAPTIVE, VAR, STATS>(p, dev, coef, var_out, fallbacks, stage, q, ring, qn, nxt, b, step, lane, wv);
+    for (; g < nbatch; g += step)
+        fdct8_batch<ADAPTIVE, VAR, STATS>(ps, dev, fallbacks, stage, qb, qc, ring, qn, nxt, g, step, lane, wv);
     if (DCTQ_ABLATE & 16) qn = 0;
-    while (qn > 0) drain_queue<ADAPTIVE, STATS>(dev, coef, q, ring, qn, lane, fallbacks);
+    while (qn > 0) drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
 }
 
 
@@ -647,17 +680,17 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneArgs p, FastT
     } while (0)
 
 template <bool A, bool V, bool S>
-static hipError_t launch_v1(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int16_t *coef,
-                            int32_t *var_num, unsigned long long *fb, hipStream_t stream) {
-    hipLaunchKernelGGL((fdct8_quant_v1<A, V, S>), dim3((p.nblk + kThreads - 1) / kThreads), dim3(kThreads), 0, stream,
-                       p, t, dev, coef, var_num, fb);
+static hipError_t launch_v1(const PlaneSet &ps, const FastTables &t, const DevTables *dev, unsigned long long *fb,
+                            hipStream_t stream) {
+    for (int k = 0; k < ps.n; ++k)
+        hipLaunchKernelGGL((fdct8_quant_v1<A, V, S>), dim3((ps.pl[k].nblk + kThreads - 1) / kThreads), dim3(kThreads),
+                           0, stream, ps.pl[k], t, dev, ps.coef[k], ps.var[k], fb);
     return hipGetLastError();
 }
 
 template <bool A, bool V, bool S>
-static hipError_t launch_v2(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int16_t *coef,
-                            int32_t *var_num, unsigned long long *fb, hipStream_t stream, int num_cus, void *ring,
-                            int ring_wgs) {
+static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTables *dev, unsigned long long *fb,
+                            hipStream_t stream, int num_cus, void *ring, int ring_wgs) {
     static int per_cu = 0;  // resident workgroups per CU for this instantiation
     if (per_cu == 0) {
         int nb = 0;
@@ -666,22 +699,22 @@ static hipError_t launch_v2(const PlaneArgs &p, const FastTables &t, const DevTa
             nb = 1;
         per_cu = nb;
     }
-    const uint32_t nbatch = ((uint32_t)p.nblk + 63u) >> 6;
+    const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
     uint32_t cap = (uint32_t)(num_cus * per_cu);
     if (cap > (uint32_t)ring_wgs) cap = (uint32_t)ring_wgs;
-    hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, p, t, dev,
-                       coef, var_num, fb, (uint4 *)ring);
+    hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps, t, dev,
+                       fb, (uint4 *)ring);
     return hipGetLastError();
 }
 
 size_t fdct8_ring_bytes(int workgroups) { return (size_t)workgroups * kWaves * kQCap * 64; }
 
-hipError_t launch_fdct8_quant(const PlaneArgs &p, const FastTables &t, const DevTables *dev, int adaptive,
-                              int16_t *coef, int32_t *var_num, unsigned long long *fallbacks, hipStream_t stream,
-                              int variant, int num_cus, void *ring, int ring_wgs) {
-    const bool a = adaptive != 0, v = var_num != nullptr, s = fallbacks != nullptr;
-    if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (p, t, dev, coef, var_num, fallbacks, stream));
-    DCTQ_SELECT(return launch_v2, a, v, s, (p, t, dev, coef, var_num, fallbacks, stream, num_cus, ring, ring_wgs));
+hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
+                              unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus, void *ring,
+                              int ring_wgs) {
+    const bool a = adaptive != 0, v = ps.var[0] != nullptr, s = fallbacks != nullptr;
+    if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
+    DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring, ring_wgs));
 }
 }  // namespace dctq

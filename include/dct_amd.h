@@ -65,6 +65,15 @@ typedef struct {
 int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num,
                        void *stream);
 
+/* The same for up to 4 planes of independent geometry (e.g. the Y, Cb, Cr planes
+ * of a 4:2:0 frame stack) in ONE launch: plane k writes coef[k] (and var_num[k]
+ * when var_num is non-NULL, in which case every var_num[k] must be set), exactly
+ * as dctq_forward_quant(plan, &planes[k], coef[k], var_num[k]) would.  Saves a
+ * launch gap and a grid tail per extra plane (the reference has no plane
+ * notion: a caller coding Y/Cb/Cr runs its per-block loop once per plane). */
+int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                              int32_t *const *var_num, void *stream);
+
 /* Forward DCT only, float coefficients coef[f][by][bx][64]
  * (|coef - dct_forward()| <= 1e-4; computed in fp64, rounded once to fp32). */
 int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream);

@@ -175,6 +175,62 @@ def test_fallback_counter_and_exactness(T, dm):
     assert ties <= n < ties + 0.05 * by * bx, (n, ties)
 
 
+def _step_blocks(rng, by, bx):
+    """Left/right two-level blocks: a quarter of their DCs are exact rounding ties at q50."""
+    ab = rng.integers(0, 256, (by, bx, 2), dtype=np.uint8)
+    blk = np.concatenate([np.repeat(ab[:, :, :1, None], 4, 3).repeat(8, 2),
+                          np.repeat(ab[:, :, 1:, None], 4, 3).repeat(8, 2)], axis=3)
+    return np.ascontiguousarray(blk.transpose(0, 2, 1, 3).reshape(by * 8, bx * 8))
+
+
+def test_forward_quant_planes(T, dm):
+    """One launch over up to 4 planes of different geometry (ragged block counts, a
+    multi-frame stack, a single block) equals per-plane calls and the oracle,
+    including var_num and tie-heavy planes whose exact-path entries share a queue."""
+    import oracle as O
+    rng = np.random.default_rng(21)
+    sets = [
+        [O.synth_plane(1, 0, 8 * 65, 8 * 9), _step_blocks(rng, 7, 13),
+         O.synth_plane(2, 3, 8, 8), _step_blocks(rng, 33, 61)],
+        [_step_blocks(rng, 40, 40), O.synth_plane(3, 1, 8 * 20, 8 * 12)],
+        [O.synth_plane(4, 0, 8 * 129, 8 * 3)],
+    ]
+    for q, ad in [(50, 0), (50, 1), (90, 0), (7, 1)]:
+        plan = dm.Plan(q, ad)
+        for planes in sets:
+            gp = [gpu_px(T, p) for p in planes]
+            vns = [T.zeros(p.size // 64, dtype=T.int32, device="cuda") for p in planes]
+            outs = plan.forward_quant_planes(gp, var_nums=vns)
+            for p, o, v in zip(planes, outs, vns):
+                assert np.array_equal(o.cpu().numpy(), O.forward_plane(p, q, ad)), (q, ad, p.shape)
+                assert np.array_equal(v.cpu().numpy().astype(np.float64) / 4096.0, O.plane_variance(p))
+            outs2 = plan.forward_quant_planes(gp)  # no var_num
+            for p, o in zip(planes, outs2):
+                assert np.array_equal(o.cpu().numpy(), O.forward_plane(p, q, ad)), (q, ad, p.shape)
+    # a frame stack as one of the planes
+    F, H, W = 3, 24, 40
+    stack = np.stack([O.synth_plane(50 + f, f % 4, W, H) for f in range(F)])
+    luma = O.synth_plane(60, 0, 8 * 31, 8 * 5)
+    outs = dm.Plan(75, 1).forward_quant_planes([gpu_px(T, stack), gpu_px(T, luma)])
+    want = np.concatenate([O.forward_plane(stack[f], 75, 1) for f in range(F)])
+    assert np.array_equal(outs[0].cpu().numpy(), want)
+    assert np.array_equal(outs[1].cpu().numpy(), O.forward_plane(luma, 75, 1))
+    # argument checks: 0 or 5 planes, a NULL var_num entry
+    g = gpu_px(T, luma)
+    plan = dm.Plan(50, 0)
+    with pytest.raises(dm.DctqError):
+        plan.forward_quant_planes([g] * 5)
+    with pytest.raises(dm.DctqError):
+        plan.forward_quant_planes([])
+    L = dm.lib()
+    d = (dm._Plane * 1)(dm.plane_desc(g))
+    o = T.empty((luma.size // 64, 64), dtype=T.int16, device="cuda")
+    cp = (C.c_void_p * 1)(o.data_ptr())
+    vp = (C.c_void_p * 1)(None)
+    rc = L.dctq_forward_quant_planes(plan._h, d, 1, C.cast(cp, C.c_void_p), C.cast(vp, C.c_void_p), None)
+    assert rc != 0
+
+
 def test_forward_float_tolerance(T, dm, tiles):
     import oracle as O
     for kind in ["uniform", "smooth", "const", "extreme"]:

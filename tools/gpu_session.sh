@@ -25,11 +25,12 @@ for step in "$@"; do
     testall) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu ;;
-    pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
-    pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
-    pmcsq) run pmcsq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
-    pmcsq2) run pmcsq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU -d $OUT/pmc_sq2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu ;;
+    benchpp) run benchpp 300 bash -c "python bench.py --steps 20 --warmup 3 --no-cpu --round-trip-steps 0 --per-plane && python bench.py --steps 20 --warmup 3 --no-cpu --round-trip-steps 0 && python bench.py --steps 20 --warmup 3 --no-cpu --round-trip-steps 0 --per-plane && python bench.py --steps 20 --warmup 3 --no-cpu --round-trip-steps 0" ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu --round-trip-steps 0 ;;
+    pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --round-trip-steps 0 ;;
+    pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --round-trip-steps 0 ;;
+    pmcsq) run pmcsq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --round-trip-steps 0 ;;
+    pmcsq2) run pmcsq2 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU -d $OUT/pmc_sq2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu --round-trip-steps 0 ;;
     rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 --frames 16 --no-cpu --backend gloo ;;
     list) run list 120 rocprofv3 -L ;;
     traffic) run traffic 60 bash -c "python tools/pmc_traffic.py $OUT/pmc_fetch/run_counter_collection.csv $OUT/pmc_write/run_counter_collection.csv --frames 64 --kind uniform -o $OUT/traffic.json && cp $OUT/traffic.json profiles/traffic.json" ;;
@@ -40,8 +41,15 @@ for step in "$@"; do
     pmcv2b) run pmcv2b 600 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA -d $OUT/pmc_v2b -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 4 ;;
     abb) run abb 300 python tools/ab_bench.py --variants 2 --b2b 20 ;;
     ceil) run ceil 120 tools/ubench/stream_ceiling ;;
+    ceil2) run ceil2 120 tools/ubench/stream_ceiling2 ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
+    pmcq1) run pmcq1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_q1 -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 3 ;;
+    pmcq2) run pmcq2 600 rocprofv3 --pmc SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_WAIT_INST_LDS -d $OUT/pmc_q2 -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 3 ;;
+    pmcs1) run pmcs1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_s1 -o run --output-format csv -- tools/ubench/stream_ceiling2 ;;
+    pmcs2) run pmcs2 600 rocprofv3 --pmc SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_WAIT_INST_LDS -d $OUT/pmc_s2 -o run --output-format csv -- tools/ubench/stream_ceiling2 ;;
+    pmca1) run pmca1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_a1 -o run --output-format csv -- python tools/aux_bench.py 16 ;;
+    pmca2) run pmca2 600 rocprofv3 --pmc SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM SQ_WAIT_INST_LDS -d $OUT/pmc_a2 -o run --output-format csv -- python tools/aux_bench.py 16 ;;
     ab23) run ab23 300 bash -c "python tools/ab_bench.py --variants 2,3 --rounds 12 && python tools/ab_bench.py --variants 2,3 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3 --rounds 6 --kind const && python tools/ab_bench.py --variants 2,3 --rounds 6 --adaptive 1 && python tools/ab_bench.py --variants 2,3 --rounds 6 --quality 90" ;;
     ab234) run ab234 300 bash -c "python tools/ab_bench.py --variants 2,3,4 --rounds 12 && python tools/ab_bench.py --variants 2,3,4 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3,4 --rounds 6 --kind const" ;;
     ab) run ab 300 python tools/ab_bench.py --variants 1,2 ;;

@@ -31,16 +31,18 @@ def main():
     ap.add_argument("--frames", type=int, required=True)
     ap.add_argument("--kind", required=True)
     ap.add_argument("--kernel", default="fdct8_quant_v2")
+    ap.add_argument("--launches", type=int, default=1, help="forward-quant dispatches per bench step")
     ap.add_argument("-o", "--out", default="profiles/traffic.json")
     a = ap.parse_args()
     f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
-    if not f or not w or len(f) % 2 or len(w) % 2:
-        raise SystemExit(f"expected luma/chroma dispatch pairs, got {len(f)} fetch / {len(w)} write")
+    if not f or not w or len(f) % a.launches or len(w) % a.launches:
+        raise SystemExit(f"expected groups of {a.launches} dispatches, got {len(f)} fetch / {len(w)} write")
     rd = 2 * statistics.mean(f) * 1024
     wr = statistics.mean(w) * 1024
-    blocks = a.frames * (480 * 270 + 2 * 240 * 135) / 2  # average blocks per launch
+    blocks = a.frames * (480 * 270 + 2 * 240 * 135) / a.launches  # average blocks per launch
     out = {"kernel": a.kernel, "frames": a.frames, "kind": a.kind, "dispatches": len(f),
+           "launches_per_step": a.launches,
            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
            "algorithmic_bytes_per_launch": 192 * blocks, "traffic_over_algorithmic": (rd + wr) / (192 * blocks),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
