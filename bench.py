@@ -13,7 +13,8 @@ times the two-launch form), int16 coefficients bit-exact with the reference.  N>
 each rank its own F frames (weak scaling, no data-path collective); value =
 all blocks / max-over-ranks wall time.  A separately reported leg
 ("round_trip", BASELINE configs[4]) runs forward DCT+quant then dequant+IDCT
-over the same frames and reports end-to-end blocks/s and PSNR.  At N>1 a
+over the same frames in ONE fused launch (dctq_round_trip_planes) and reports
+end-to-end blocks/s (the unfused two-kernel pair timed beside it) and PSNR.  At N>1 a
 second, separately reported leg ("gather") times forward DCT+quant of the luma frames followed by the RCCL
 all-gather of every rank's int16 coefficient planes (BASELINE configs[3],
 SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange.
@@ -129,52 +130,62 @@ def gather_leg(args, plan, luma, coef_y, world, rank, dev):
 
 def round_trip_leg(args, plan, luma, chroma, world, dev):
     """BASELINE configs[4]: forward DCT+quant then dequant+IDCT of every plane of
-    the frame stream (unfused: dctq_forward_quant with var_num, dctq_inverse),
-    end-to-end blocks/s (max over ranks) and PSNR of the first luma frame vs its
-    input, with the reference's formula (recon clamped to [0,255],
-    tests/test_entropy.c:376-393).  Non-adaptive plans reproduce the reference's
-    1/Q dequantization (src/quantization.c:139,144), hence their low PSNR."""
-    planes = []
-    for px in (luma, chroma):
-        f, h, w = px.shape
-        n = f * (h // 8) * (w // 8)
-        planes.append((px, torch.empty((n, 64), dtype=torch.int16, device=dev),
-                       torch.empty(n, dtype=torch.int32, device=dev),
-                       torch.empty((n, 64), dtype=torch.float32, device=dev)))
+    the frame stream, FUSED (dctq_round_trip_planes: one launch, the quantized
+    ints handed to the inverse through LDS, 448 B/block), end-to-end blocks/s
+    (max over ranks) and PSNR of the first luma frame vs its input, with the
+    reference's formula (recon clamped to [0,255], tests/test_entropy.c:376-393).
+    The unfused pair (forward_quant_planes with var_num + dctq_inverse per plane,
+    584 B/block) is timed alongside for comparison.  Non-adaptive plans reproduce
+    the reference's 1/Q dequantization (src/quantization.c:139,144), hence their
+    low PSNR."""
+    import math
+    pls = [luma, chroma]
+    nbs = [px.shape[0] * (px.shape[1] // 8) * (px.shape[2] // 8) for px in pls]
+    co = [torch.empty((n, 64), dtype=torch.int16, device=dev) for n in nbs]
+    vn = [torch.empty(n, dtype=torch.int32, device=dev) for n in nbs]
+    rec = [torch.empty((n, 64), dtype=torch.float32, device=dev) for n in nbs]
 
-    def once():
-        plan.forward_quant_planes([p[0] for p in planes], outs=[p[1] for p in planes],
-                                  var_nums=[p[2] for p in planes])
-        for px, co, vn, rec in planes:
-            plan.inverse(co, var_num=vn, out=rec)
+    def fused():
+        plan.round_trip_planes(pls, outs=co, recons=rec)
 
-    once()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.round_trip_steps):
-        once()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    nblk = sum(p[1].shape[0] for p in planes)
+    def unfused():
+        plan.forward_quant_planes(pls, outs=co, var_nums=vn)
+        for c, v, r in zip(co, vn, rec):
+            plan.inverse(c, var_num=v, out=r)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.round_trip_steps):
+            fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    el_u = timed(unfused)
+    el = timed(fused)  # last: rec holds the fused kernel's output
+    nblk = sum(nbs)
     # PSNR of luma frame 0 (block order is raster, so compare block by block)
-    px, _, _, rec = planes[0]
-    h, w = px.shape[1], px.shape[2]
+    h, w = luma.shape[1], luma.shape[2]
     n0 = (h // 8) * (w // 8)
-    orig = px[0].reshape(h // 8, 8, w // 8, 8).permute(0, 2, 1, 3).reshape(n0, 64).double()
-    mse = float(((orig - rec[:n0].double().clamp(0, 255)) ** 2).mean())
-    psnr = float("inf") if mse == 0 else 10.0 * __import__("math").log10(255.0 * 255.0 / mse)
-    bpb = 64 + 128 + 4 + 128 + 4 + 256
-    return {"op": "forward_quant_planes(var_num) + inverse per plane (unfused)", "steps": args.round_trip_steps,
+    orig = luma[0].reshape(h // 8, 8, w // 8, 8).permute(0, 2, 1, 3).reshape(n0, 64).double()
+    mse = float(((orig - rec[0][:n0].double().clamp(0, 255)) ** 2).mean())
+    psnr = float("inf") if mse == 0 else 10.0 * math.log10(255.0 * 255.0 / mse)
+    bpb = 64 + 128 + 256
+    return {"op": "round_trip_planes (fused forward+inverse, one launch per step)", "steps": args.round_trip_steps,
             "blocks_per_s": world * nblk * args.round_trip_steps / el,
             "ms_per_step": el / args.round_trip_steps * 1e3,
             "bytes_per_block": bpb, "achieved_GBs_per_gpu": nblk * bpb * args.round_trip_steps / el / 1e9,
+            "unfused_blocks_per_s": world * nblk * args.round_trip_steps / el_u,
+            "unfused_bytes_per_block": 64 + 128 + 4 + 128 + 4 + 256,
             "psnr_db_luma_frame0": psnr,
             "psnr_note": "bug-compatible 1/Q dequantization for adaptive=0 (reference semantics)"}
 

@@ -47,6 +47,7 @@ def lib() -> C.CDLL:
             "dctq_plan_set_fallback_counter": ([vp, vp], i),
             "dctq_forward_quant": ([vp, C.POINTER(_Plane), vp, vp, vp], i),
             "dctq_forward_quant_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
+            "dctq_round_trip_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, vp], i),
             "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
             "dctq_inverse": ([vp, vp, vp, ll, vp, vp], i),
             "dctq_synth": ([C.c_uint64, i, C.POINTER(_Plane), vp], i),
@@ -146,6 +147,26 @@ class Plan:
                                                C.cast(vp, C.c_void_p) if vp is not None else None,
                                                _stream_ptr(stream)))
         return outs
+
+    def round_trip_planes(self, planes, outs=None, recons=None, var_nums=None, stream=None):
+        """Fused forward + inverse of up to 4 planes in ONE launch.  Returns (coefs, recons):
+        int16 [nblk_k, 64] (== forward_quant) and float32 [nblk_k, 64]
+        (== inverse(coef, var_num) within 1e-4)."""
+        import torch
+        n = len(planes)
+        descs = (_Plane * n)(*[plane_desc(px) for px in planes])
+        nbs = [d.nframes * (d.width // 8) * (d.height // 8) for d in descs]
+        if outs is None:
+            outs = [torch.empty((nb, 64), dtype=torch.int16, device=px.device) for nb, px in zip(nbs, planes)]
+        if recons is None:
+            recons = [torch.empty((nb, 64), dtype=torch.float32, device=px.device) for nb, px in zip(nbs, planes)]
+        cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+        rp = (C.c_void_p * n)(*[r.data_ptr() for r in recons])
+        vp = (C.c_void_p * n)(*[v.data_ptr() for v in var_nums]) if var_nums is not None else None
+        _check(lib().dctq_round_trip_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
+                                            C.cast(vp, C.c_void_p) if vp is not None else None,
+                                            C.cast(rp, C.c_void_p), _stream_ptr(stream)))
+        return outs, recons
 
     def forward_float(self, px, out=None, stream=None):
         import torch

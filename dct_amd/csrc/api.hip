@@ -240,12 +240,12 @@ int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter)
     return DCTQ_OK;
 }
 
-int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
-                              int32_t *const *var_num, void *stream) {
-    DCTQ_ENTRY;
-    if (!plan || !planes || !coef) return fail(DCTQ_EINVAL, "plan/planes/coef is NULL");
+static int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num,
+                     dctq::PlaneSet *ps_out) {
+    if (!planes || !coef) return fail(DCTQ_EINVAL, "planes/coef is NULL");
     if (nplanes < 1 || nplanes > dctq::kMaxPlanes) return fail(DCTQ_EINVAL, "nplanes must be in [1, 4]");
-    dctq::PlaneSet ps = {};
+    dctq::PlaneSet &ps = *ps_out;
+    ps = {};
     ps.n = nplanes;
     uint32_t first = 0;
     for (int k = 0; k < nplanes; ++k) {
@@ -261,9 +261,35 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
     }
     ps.first[nplanes] = first;
     for (int k = nplanes + 1; k <= dctq::kMaxPlanes; ++k) ps.first[k] = first;
+    return DCTQ_OK;
+}
+
+int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                              int32_t *const *var_num, void *stream) {
+    DCTQ_ENTRY;
+    if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
+    dctq::PlaneSet ps;
+    int rc = plane_set(planes, nplanes, coef, var_num, &ps);
+    if (rc) return rc;
     HIPCHK(dctq::launch_fdct8_quant(ps, plan->fast, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
                                     plan->variant, plan->num_cus, plan->ring, plan->ring_wgs),
            "fdct8_quant launch");
+    return DCTQ_OK;
+}
+
+int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                           int32_t *const *var_num, float *const *recon, void *stream) {
+    DCTQ_ENTRY;
+    if (!plan || !recon) return fail(DCTQ_EINVAL, "plan/recon is NULL");
+    dctq::RoundTripSet rt = {};
+    int rc = plane_set(planes, nplanes, coef, var_num, &rt.ps);
+    if (rc) return rc;
+    for (int k = 0; k < nplanes; ++k) {
+        if (!recon[k] || ((uintptr_t)recon[k]) % 16) return fail(DCTQ_EINVAL, "recon[k] NULL or not 16-byte aligned");
+        rt.recon[k] = recon[k];
+    }
+    HIPCHK(dctq::launch_roundtrip(rt, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream, plan->num_cus),
+           "roundtrip launch");
     return DCTQ_OK;
 }
 

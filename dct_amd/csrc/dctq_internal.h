@@ -78,11 +78,19 @@ struct PlaneSet {
     int n;
 };
 
+// The fused round trip's planes: forward outputs as PlaneSet, plus fp32 recon per plane.
+struct RoundTripSet {
+    PlaneSet ps;
+    float *recon[kMaxPlanes];
+};
+
 hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
                               unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus, void *ring,
                               int ring_wgs);
 // bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
 size_t fdct8_ring_bytes(int workgroups);
+hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
+                            hipStream_t stream, int num_cus);
 hipError_t launch_fdct8_float_pair(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream,
                                    int num_cus);
 hipError_t launch_idct8_pair(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,

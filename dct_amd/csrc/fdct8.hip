@@ -21,67 +21,9 @@
 // contraction: this file is compiled with -ffp-contract=off), with IEEE
 // division and round-half-away-from-zero.  All other coefficients are provably
 // rounded the same way the reference rounds them.
-#include "dctq_internal.h"
-#include "fdct8_bound.h"
+#include "fdct8_core.h"
 
 namespace dctq {
-
-constexpr int kWaves = 4;
-constexpr int kThreads = 64 * kWaves;
-constexpr int kPitch = 9;  // uint4 per block in the LDS stage: 128 B + 16 B pad
-constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23: fma(y, w, kMagic) rounds y*w to an integer in its low bits
-
-__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
-
-// The 8-point AAN flow graph, operation for operation tools/aan_model.py::aan8
-// (the model tools/guard_bound.py bounds).  Outputs y_k with X_k = kAanScale[k]*y_k.
-template <typename T>
-__device__ __forceinline__ void aan8(T &v0, T &v1, T &v2, T &v3, T &v4, T &v5, T &v6, T &v7, T c4, T c6,
-                                     T c2mc6, T c2pc6) {
-    T a0 = v0 + v7, b0 = v0 - v7;
-    T a1 = v1 + v6, b1 = v1 - v6;
-    T a2 = v2 + v5, b2 = v2 - v5;
-    T a3 = v3 + v4, b3 = v3 - v4;
-    T e0 = a0 + a3, e3 = a0 - a3;
-    T e1 = a1 + a2, e2 = a1 - a2;
-    T y0 = e0 + e1, y4 = e0 - e1;
-    T m = (e2 + e3) * c4;
-    T y2 = e3 + m, y6 = e3 - m;
-    T o0 = b3 + b2;
-    T o1 = b2 + b1;
-    T o2 = b1 + b0;
-    T z5 = (o0 - o2) * c6;
-    T z2 = fma_t(c2mc6, o0, z5);
-    T z4 = fma_t(c2pc6, o2, z5);
-    T z3 = o1 * c4;
-    T z11 = b0 + z3, z13 = b0 - z3;
-    v0 = y0;
-    v1 = z11 + z4;
-    v2 = y2;
-    v3 = z13 - z2;
-    v4 = y4;
-    v5 = z13 + z2;
-    v6 = y6;
-    v7 = z11 - z4;
-}
-
-template <typename T>
-__device__ __forceinline__ void aan8x8(T (&v)[8][8], T c4, T c6, T c2mc6, T c2pc6) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) aan8(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7], c4, c6, c2mc6, c2pc6);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) aan8(v[0][c], v[1][c], v[2][c], v[3][c], v[4][c], v[5][c], v[6][c], v[7][c], c4, c6, c2mc6, c2pc6);
-}
-
-// Locate the lane's block: n -> (frame, by, bx) -> pointer to its top-left pixel.
-__device__ __forceinline__ const uint8_t *block_ptr(const PlaneArgs &p, uint32_t n) {
-    uint32_t f = fdiv(n, p.div_frame);
-    uint32_t rem = n - f * (uint32_t)p.nblk_frame;
-    uint32_t by = fdiv(rem, p.div_bw);
-    uint32_t bx = rem - by * (uint32_t)p.bw;
-    return p.src + (long long)f * p.frame_stride + (long long)(by * 8) * p.stride + (long long)bx * 8;
-}
 
 // Reference-order fp64 recomputation of ONE quantized coefficient c = 8i + j:
 //   temp[k][j] = sum_l x[k][l] * D^T[l][j]      (src/dct.c:57-64, l ascending)
@@ -108,15 +50,6 @@ __device__ __forceinline__ int exact_quant(const uint8_t *__restrict__ px, long 
         out += dct[i * 8 + k] * t;
     }
     return (int)round(out / m);
-}
-
-// src/quantization.c:171-211 for is_quantize=1, element c, given the block's
-// exact variance (var_num / 4096): nv = fmin(1, fmax(0.1, var/1000)),
-// M = Q*(2-nv) clamped to >= 1, DC keeps Q.
-__device__ __forceinline__ double adaptive_scale(int32_t var_num) {
-    const double var = (double)var_num / 4096.0;  // == (sum_sq/64) - mean*mean exactly
-    const double nv = fmin(1.0, fmax(0.1, var / 1000.0));
-    return 2.0 - nv;
 }
 
 template <bool ADAPTIVE, bool VAR, bool STATS>
@@ -265,124 +198,20 @@ __global__ __launch_bounds__(kThreads) void fdct8_quant_v1(PlaneArgs p, FastTabl
 //    clips the tail, so the stores are unconditional);
 //  * flagged (block, coefficient) pairs go to a wave-local LDS queue and are
 //    recomputed exactly 64 at a time (every lane busy), then patched in HBM.
-typedef float f2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-constexpr int kQCap = 128;     // per-wave tie queue: < 64 between rounds + one round of <= 64
-constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) conflicts for the b32 writes
-#ifndef DCTQ_STORE_AUX
-// Cache policy of the bulk coefficient stores (gfx950: 1 sc0, 2 nt, 16 sc1).
-// Non-temporal: -15 % kernel time on the 4K stream (profiles/r01/store_policy.md);
-// the written lines are never re-read by this kernel except by tie patches,
-// which come after a vmcnt(0).
-#define DCTQ_STORE_AUX 2
-#endif
-#ifndef DCTQ_LOAD_NT
-#define DCTQ_LOAD_NT 1  // pixel rows are read exactly once
-#endif
-#ifndef DCTQ_ABLATE
-#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores
-#endif
-
-template <int K>
-__device__ __forceinline__ float cvt_ubyte(uint32_t w) {
-    float f;
-    if constexpr (K == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(w));
-    else if constexpr (K == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(w));
-    else if constexpr (K == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(w));
-    else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(w));
-    return f;
-}
-
-// Pixel rows are read exactly once: non-temporal loads (+8.7 % on the memory
-// ceiling of this stream, profiles/r01/valu_issue_rates.md).
-__device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 (&rows)[8]) {
-    if (DCTQ_ABLATE & 64) {  // diagnostic: opaque synthetic rows, no memory traffic
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            uint32_t a = n * 0x9E3779B1u + r, c = a ^ (a >> 13);
-            asm volatile("" : "+v"(a), "+v"(c));
-            rows[r] = make_uint2(a, c);
-        }
-        return;
-    }
-    const uint8_t *px = block_ptr(p, n < (uint32_t)p.nblk ? n : 0);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-#if DCTQ_LOAD_NT
-        const u2v t = __builtin_nontemporal_load(reinterpret_cast<const u2v *>(px + r * p.stride));
-        rows[r] = make_uint2(t.x, t.y);
-#else
-        rows[r] = *reinterpret_cast<const uint2 *>(px + r * p.stride);
-#endif
-    }
-}
-
 // Exact reference-order quantization of coefficient c of the block at px (one
-// queue entry): the arithmetic of exact_quant() above plus, for adaptive plans,
-// the block's exact variance and adjusted divisor (src/quantization.c:153-211).
+// queue entry): exact_from_rows() over the pixels stashed when it was queued.
 // A drain runs 64 of these at once (one per lane), so latency matters: all 8
-// pixel rows and the 16 table entries are requested before the fp64 chain.
+// pixel rows are requested before the fp64 chain.
 template <bool ADAPTIVE>
 __device__ int exact_entry(const uint4 *__restrict__ stash, int c, const DevTables *__restrict__ dev) {
-    const int i = c >> 3, j = c & 7;
     uint2 rows[8];
-    double dj[8], di[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint4 w = stash[k];  // rows 2k, 2k+1 of the block, stashed when the entry was queued
+        const uint4 w = stash[k];  // rows 2k, 2k+1 of the block
         rows[2 * k] = make_uint2(w.x, w.y);
         rows[2 * k + 1] = make_uint2(w.z, w.w);
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        dj[k] = dev->dct[j * 8 + k];  // D^T[k][j]
-        di[k] = dev->dct[i * 8 + k];  // D[i][k]
-    }
-    double m = dev->quant[c];
-    if (ADAPTIVE && c != 0) {
-        uint32_t s1 = 0, s2 = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            s1 = __builtin_amdgcn_udot4(rows[k].x, 0x01010101u, s1, false);
-            s1 = __builtin_amdgcn_udot4(rows[k].y, 0x01010101u, s1, false);
-            s2 = __builtin_amdgcn_udot4(rows[k].x, rows[k].x, s2, false);
-            s2 = __builtin_amdgcn_udot4(rows[k].y, rows[k].y, s2, false);
-        }
-        const int32_t sx = (int32_t)s1 - 8192;
-        const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
-        m = m * adaptive_scale(64 * sxx - sx * sx);
-        if (m < 1.0) m = 1.0;
-    }
-    // temp[k][j] = sum_l x[k][l] D^T[l][j]; out = sum_k D[i][k] temp[k][j]  (src/dct.c:57-74)
-    double out = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        double t = 0.0;
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            const uint32_t w = l < 4 ? rows[k].x : rows[k].y;
-            t += ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
-        }
-        out += di[k] * t;
-    }
-    return (int)round(out / m);
-}
-
-// Coefficient output of plane k (k wave-uniform or not: a select chain, no indexed kernarg loads).
-__device__ __forceinline__ int16_t *coef_of(const PlaneSet &ps, uint32_t k) {
-    int16_t *c = ps.coef[0];
-#pragma unroll
-    for (int i = 1; i < kMaxPlanes; ++i) c = k == (uint32_t)i ? ps.coef[i] : c;
-    return c;
-}
-
-// Plane of global batch g (wave-uniform).
-__device__ __forceinline__ int plane_of(const PlaneSet &ps, uint32_t g) {
-    int k = 0;
-#pragma unroll
-    for (int i = 1; i < kMaxPlanes; ++i) k += (i < ps.n && g >= ps.first[i]) ? 1 : 0;
-    return k;
+    return exact_from_rows<ADAPTIVE>(rows, c, dev);
 }
 
 // Exact recomputation of up to 64 queued (block, coefficient) entries, one per
@@ -404,103 +233,6 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
     qn -= take;
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // nothing of this rare path stays in flight
-}
-
-// The arithmetic of one 64-block batch (one block per lane): u8 rows -> fp32,
-// exact variance numerator, AAN row pass, column pairs fused with quantization
-// into the wave's LDS stage, tie masks (bit 31 - p%32 of mlo/mhi = processing
-// slot p = 16*cp + 2*i + h needs the exact path).
-template <bool ADAPTIVE, bool VAR>
-__device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev, const uint2 (&cur)[8], uint4 *stage,
-                                              int lane, int wv, uint32_t &mlo, uint32_t &mhi, int32_t &var_num) {
-    const f2 M2 = {kMagic, kMagic};
-    float v[8][8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        v[r][0] = cvt_ubyte<0>(cur[r].x);
-        v[r][1] = cvt_ubyte<1>(cur[r].x);
-        v[r][2] = cvt_ubyte<2>(cur[r].x);
-        v[r][3] = cvt_ubyte<3>(cur[r].x);
-        v[r][4] = cvt_ubyte<0>(cur[r].y);
-        v[r][5] = cvt_ubyte<1>(cur[r].y);
-        v[r][6] = cvt_ubyte<2>(cur[r].y);
-        v[r][7] = cvt_ubyte<3>(cur[r].y);
-    }
-    var_num = 0;
-    if (ADAPTIVE || VAR) {
-        uint32_t s1 = 0, s2 = 0;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            s1 = __builtin_amdgcn_udot4(cur[r].x, 0x01010101u, s1, false);
-            s1 = __builtin_amdgcn_udot4(cur[r].y, 0x01010101u, s1, false);
-            s2 = __builtin_amdgcn_udot4(cur[r].x, cur[r].x, s2, false);
-            s2 = __builtin_amdgcn_udot4(cur[r].y, cur[r].y, s2, false);
-        }
-        const int32_t sx = (int32_t)s1 - 8192;
-        const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
-        var_num = 64 * sxx - sx * sx;
-    }
-
-    // ---- row pass, then column pairs fused with quantization
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-        if (!(DCTQ_ABLATE & 2))
-            aan8(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7], DCTQ_C4, DCTQ_C6,
-                 DCTQ_C2MC6, DCTQ_C2PC6);
-
-    f2 sc2 = {1.0f, 1.0f};
-    if (ADAPTIVE) {
-        const float inv = (float)(1.0 / adaptive_scale(var_num));
-        sc2 = f2{inv, inv};
-    }
-    // Per-plan tables through an opaque per-batch pointer in the constant address
-    // space: scalar loads stay inside the loop (hoisted, they would need 128 live
-    // SGPRs) and stay scalar (a generic pointer becomes flat_load + vmcnt(0)).
-    const FastTables *tg = &dev->fast;
-    asm volatile("" : "+s"(tg));
-    const __attribute__((address_space(4))) FastTables *tp = (const __attribute__((address_space(4))) FastTables *)tg;
-    mlo = 0;
-    mhi = 0;  // bit (31 - p%32): processing slot p = 16*cp + 2*i + h flagged
-    uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
-#pragma unroll
-    for (int cp = 0; cp < 4; ++cp) {
-        const int c0 = 2 * cp;
-        if (!(DCTQ_ABLATE & 2)) {
-            aan8(v[0][c0], v[1][c0], v[2][c0], v[3][c0], v[4][c0], v[5][c0], v[6][c0], v[7][c0], DCTQ_C4, DCTQ_C6,
-                 DCTQ_C2MC6, DCTQ_C2PC6);
-            aan8(v[0][c0 + 1], v[1][c0 + 1], v[2][c0 + 1], v[3][c0 + 1], v[4][c0 + 1], v[5][c0 + 1], v[6][c0 + 1],
-                 v[7][c0 + 1], DCTQ_C4, DCTQ_C6, DCTQ_C2MC6, DCTQ_C2PC6);
-        }
-        if (cp == 0) v[0][0] -= 8192.0f;  // 64 * 128: exact (integer < 2^24)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int c = i * 8 + c0, slot = 16 * cp + 2 * i;
-            const f2 y = {v[i][c0], v[i][c0 + 1]};
-            f2 w = (DCTQ_ABLATE & 256) ? f2{0.0625f + slot * 1e-3f, 0.0625f} : f2{tp->ws[slot], tp->ws[slot + 1]};
-            if (ADAPTIVE) {
-                if (c == 0) w.y *= sc2.y;  // the DC keeps Q (src/quantization.c:198-199)
-                else w *= sc2;
-            }
-            const f2 tt = __builtin_elementwise_fma(y, w, M2);
-            const f2 nr = M2 - tt;
-            const f2 f = __builtin_elementwise_fma(y, w, nr);
-            const f2 T = (DCTQ_ABLATE & 256) ? f2{0.25f, 0.25f} : f2{tp->t2s[slot], tp->t2s[slot + 1]};
-            const f2 d = __builtin_elementwise_fma(-f, f, T);  // < 0  <=>  |f| beyond the guard
-            if (DCTQ_ABLATE & 1) {
-            } else if (cp < 2) {
-                mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.x), 31);
-                mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.y), 31);
-            } else {
-                mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.x), 31);
-                mhi = __builtin_amdgcn_alignbit(mhi, __float_as_uint(d.y), 31);
-            }
-            st32[i * 4 + cp] = __builtin_amdgcn_perm(__float_as_uint(tt.y), __float_as_uint(tt.x), 0x05040100u);
-        }
-        // Pin the flag mask here: otherwise LLVM sinks the 32 residual tests of
-        // this column pair to their only use (the queue phase, after the stores)
-        // and keeps every residual live across the stores.
-        asm volatile("" : "+v"(mlo), "+v"(mhi));
-    }
 }
 
 // One 64-block batch of the v2 loop.  `nxt` holds this batch's rows on entry and
@@ -531,20 +263,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     int32_t var_num;
     fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
 
-    // A flagged DC of a CONSTANT block (flat image areas: an exact .5 tie for
-    // half of all pixel values at q50) is resolved from the plan's table of
-    // reference-order DCs instead of the exact path.  Checked only when some
-    // lane's DC (processing slot 0 = bit 31 of mlo) is flagged.
-    if (!(DCTQ_ABLATE & 8) && __builtin_amdgcn_ballot_w64((mlo >> 31) != 0u)) {
-        const uint32_t w = cur[0].x;
-        bool flat = w == (w & 0xFFu) * 0x01010101u;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) flat &= (cur[r].x == w) & (cur[r].y == w);  // bitwise: no short-circuit branches
-        if ((mlo >> 31) && flat) {
-            reinterpret_cast<int16_t *>(stage)[(wv * 64 + lane) * (kPitch2 / 2)] = dev->dc_const[w & 0xFFu];
-            mlo &= 0x7FFFFFFFu;
-        }
-    }
+    flat_dc_fix(dev, cur, stage, lane, wv, mlo);
 
     // Consume the prefetched rows HERE, before this batch's stores are issued:
     // the wait the compiler puts in front of this fence then covers loads issued
@@ -603,17 +322,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
             else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
         }
         if (mlo | mhi) {
-            int slot;
-            if (mlo) {
-                slot = __clz(mlo);
-                mlo &= ~(0x80000000u >> slot);
-            } else {
-                const int z = __clz(mhi);
-                mhi &= ~(0x80000000u >> z);
-                slot = 32 + z;
-            }
-            // slot = 16*cp + 2*i + h  ->  coefficient 8*i + 2*cp + h
-            const int c = (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
+            const int c = pop_flag(mlo, mhi);
             const uint32_t pos =
                 qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
             qb[pos] = n;

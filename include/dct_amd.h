@@ -74,6 +74,18 @@ int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *co
 int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               int32_t *const *var_num, void *stream);
 
+/* Fused round trip (BASELINE configs[4]) of up to 4 planes in ONE launch: for
+ * plane k, coef[k] (and var_num[k] if var_num is non-NULL) exactly as
+ * dctq_forward_quant_planes, and
+ *   recon[k][b][64] = dct_inverse(dequantize(coef[k][b])) + 128
+ * exactly as dctq_inverse(plan, coef[k], var_num[k], ...) would produce it
+ * (float, unclamped, |err| <= 1e-4).  The quantized ints go from the forward to
+ * the inverse through LDS: 448 B of HBM traffic per block instead of 584 B for
+ * the two calls.  var_num is optional even for adaptive plans.  recon 16-byte
+ * aligned. */
+int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                           int32_t *const *var_num, float *const *recon, void *stream);
+
 /* Forward DCT only, float coefficients coef[f][by][bx][64]
  * (|coef - dct_forward()| <= 1e-4; computed in fp64, rounded once to fp32). */
 int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream);
@@ -107,7 +119,7 @@ int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long 
 
 /* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented
  * by the number of coefficients resolved by the exact fp64 tie path in later
- * dctq_forward_quant calls on this plan (costs one atomic per affected wave). */
+ * dctq_forward_quant / _planes / dctq_round_trip_planes calls on this plan (costs one atomic per affected wave). */
 int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter);
 
 /* Synthetic frames (counter-based splitmix64; identical to the oracle's

@@ -280,6 +280,62 @@ def test_float_and_inverse_ragged_geometries(T, dm):
             assert np.abs(rec - want).max() <= 1e-4, (w, h, nf, q, ad)
 
 
+def test_round_trip_planes_fused(T, dm):
+    """dctq_round_trip_planes (one launch, forward + inverse fused through LDS):
+    coefficients bit-exact with the oracle, recon within 1e-4 of the oracle's
+    dct_inverse(dequantize()), over ragged planes (block counts not multiples of
+    32/64), a frame stack, tie-heavy step-block planes (exact path inside the
+    fused kernel) and adaptive plans; var_num optional."""
+    import oracle as O
+    rng = np.random.default_rng(33)
+    planes = [O.synth_plane(5, 0, 8 * 65, 8 * 9), _step_blocks(rng, 7, 13), O.synth_plane(6, 1, 8, 8),
+              _step_blocks(rng, 17, 47)]
+    F, H, W = 3, 24, 40
+    stack = np.stack([O.synth_plane(80 + f, f % 4, W, H) for f in range(F)])
+    for q, ad in [(50, 0), (50, 1), (90, 1), (10, 0), (100, 1)]:
+        plan = dm.Plan(q, ad)
+        for ps in (planes, [stack, planes[0]]):
+            gp = [gpu_px(T, p) for p in ps]
+            vns = [T.zeros(p.size // 64, dtype=T.int32, device="cuda") for p in ps]
+            coefs, recs = plan.round_trip_planes(gp, var_nums=vns)
+            coefs2, recs2 = plan.round_trip_planes(gp)
+            for p, c, r, v, c2, r2 in zip(ps, coefs, recs, vns, coefs2, recs2):
+                frames = list(p) if p.ndim == 3 else [p]
+                want_c = np.concatenate([O.forward_plane(f, q, ad) for f in frames])
+                want_v = np.concatenate([O.plane_variance(f) for f in frames])
+                got_c = c.cpu().numpy()
+                assert np.array_equal(got_c, want_c), (q, ad, p.shape)
+                assert np.array_equal(c2.cpu().numpy(), want_c)
+                assert np.array_equal(v.cpu().numpy().astype(np.float64) / 4096.0, want_v)
+                want_r = O.inverse_plane(want_c, q, ad, want_v if ad else None) + 128.0
+                err = np.abs(r.cpu().numpy().astype(np.float64) - want_r).max()
+                assert err <= 1e-4, (q, ad, p.shape, err)
+                assert np.array_equal(r.cpu().numpy(), r2.cpu().numpy())
+                # and the same floats as the unfused dctq_inverse
+                ri = plan.inverse(c, var_num=v).cpu().numpy()
+                assert np.abs(ri - r.cpu().numpy()).max() <= 2e-5
+
+
+def test_round_trip_exact_count_matches_forward(T, dm):
+    """The fused kernel resolves ties in place; it recomputes exactly the
+    coefficients the forward kernel sends to its deferred queue."""
+    rng = np.random.default_rng(8)
+    px = gpu_px(T, _step_blocks(rng, 48, 96))
+    counts = []
+    for fused in (False, True):
+        plan = dm.Plan(50, 0)
+        cnt = T.zeros(1, dtype=T.int64, device="cuda")
+        plan.set_fallback_counter(cnt)
+        if fused:
+            plan.round_trip_planes([px])
+        else:
+            plan.forward_quant(px)
+        T.cuda.synchronize()
+        counts.append(int(cnt.item()))
+        plan.set_fallback_counter(None)
+    assert counts[0] == counts[1] and counts[0] > 100, counts
+
+
 def test_example_block_pipeline(T, dm, blocks):
     """tests/test_entropy.c:290-393 example block through the batched API."""
     from golden.make_golden import EXAMPLE
