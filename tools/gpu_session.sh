@@ -42,6 +42,7 @@ for step in "$@"; do
     abb) run abb 300 python tools/ab_bench.py --variants 2 --b2b 20 ;;
     ceil) run ceil 120 tools/ubench/stream_ceiling ;;
     ceil2) run ceil2 120 tools/ubench/stream_ceiling2 ;;
+    ceil3) run ceil3 120 tools/ubench/stream_ceiling3 ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
     rtb) run rtb 300 bash -c "python tools/rt_bench.py 64 && python tools/rt_bench.py 64 --adaptive" ;;
