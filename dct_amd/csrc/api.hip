@@ -363,7 +363,8 @@ int dctq_rle_count(const int16_t *coef, long long nblocks, uint32_t *offsets, vo
     DCTQ_ENTRY;
     if (int rc = rle_args(coef, offsets, nblocks)) return rc;
     if (!workspace) return fail(DCTQ_EINVAL, "workspace is NULL");
-    HIPCHK(dctq::launch_rle_count(coef, nblocks, offsets, workspace, (hipStream_t)stream), "rle_count launch");
+    HIPCHK(dctq::launch_rle_count(coef, nblocks, offsets, workspace, (hipStream_t)stream, device_cus()),
+           "rle_count launch");
     return DCTQ_OK;
 }
 

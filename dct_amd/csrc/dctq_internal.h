@@ -96,7 +96,8 @@ hipError_t launch_fdct8_float_pair(const PlaneArgs &p, const DevTables *dev, flo
 hipError_t launch_idct8_pair(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
                              long long nblk, float *recon, hipStream_t stream, int num_cus);
 size_t rle_workspace_bytes(long long nblk);
-hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offsets, void *ws, hipStream_t stream);
+hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offsets, void *ws, hipStream_t stream,
+                            int num_cus);
 hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,
                            hipStream_t stream, int num_cus);
 hipError_t launch_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblk, int16_t *coef,

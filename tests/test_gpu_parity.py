@@ -560,3 +560,19 @@ def test_rle_bit_exact_and_round_trip(T, dm):
         s = sym.cpu().numpy().view(np.uint32)
         assert ((s & 0xFFFF).astype(np.uint16).view(np.int16).tolist(), (s >> 16).tolist()) == \
             (b["values"], b["runs"]), name
+
+
+def test_rle_large_planes(T, dm):
+    """Block counts past one tile-scan chunk (8192 tiles = 524 288 blocks) and
+    with a ragged last tile: 5 4K luma frames plus 37 blocks, several tiles per
+    wave in the count pass, every offset and symbol against the oracle."""
+    import oracle as O
+    px = dm.synth(31, "uniform", 3840, 2160, 5)
+    coef = dm.Plan(50, 0).forward_quant(px)
+    extra = T.from_numpy(O.forward_plane(O.synth_plane(32, 1, 8 * 37, 8), 50, 0)).cuda()
+    c = T.cat([coef, extra]).contiguous()
+    off, sym = dm.rle_encode(c)
+    woff, wsym = O.rle_encode_plane(c.cpu().numpy())
+    assert np.array_equal(off.cpu().numpy().view(np.uint32), woff)
+    assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym)
+    assert np.array_equal(dm.rle_decode(sym, off).cpu().numpy(), c.cpu().numpy())

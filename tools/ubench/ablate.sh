@@ -3,10 +3,11 @@
 # removed (outputs are WRONG in these builds): tools/ubench/libablate_<mask>.so
 set -e
 cd "$(dirname "$0")/../.."
+srcs=$(python -c "import dct_amd.build as b; print(' '.join('dct_amd/csrc/' + s for s in b.SOURCES))")
 for m in ${@:-8 16 32}; do
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-slp-vectorize \
     -Wno-unused-command-line-argument -DDCTQ_ABLATE=$m -Iinclude -Idct_amd/csrc \
-    dct_amd/csrc/api.hip dct_amd/csrc/legacy.hip dct_amd/csrc/fdct8.hip dct_amd/csrc/fdct8_aux.hip dct_amd/csrc/f64_pair.hip dct_amd/csrc/rle.hip \
+    $srcs \
     -o tools/ubench/libablate_$m.so &
 done
 wait
