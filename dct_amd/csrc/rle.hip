@@ -34,6 +34,7 @@ __constant__ uint8_t kUnzigzag[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,
 
 constexpr int kRleWaves = 4;
 constexpr int kRleThreads = 64 * kRleWaves;
+constexpr int kGroup = 8;  // decode: blocks whose symbol loads are in flight together
 
 __device__ __forceinline__ uint64_t lane_mask_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
@@ -94,205 +95,242 @@ __global__ __launch_bounds__(kRleThreads) void rle_count_kernel(const int16_t *_
     }
 }
 
-// ---- exclusive scan of the tile totals in place (one workgroup of 1024), total -> *total_out.
-// Chunks of 8192 totals: each thread scans 8 consecutive values (two 16-B loads,
-// coalesced), a wave scan and a 16-entry LDS scan combine the threads, the
-// running carry crosses chunks; the next chunk's loads are issued first.
+// ---- exclusive scan of the tile totals in place, segment by segment: one
+// workgroup of 1024 per segment of 8192 tiles (each thread scans 8 consecutive
+// totals from two 16-B loads, a wave scan and a 16-entry LDS pass combine the
+// threads); the segment's sum -> segs[s].  The segments' own prefix is added in
+// the fix-up, which also writes the grand total.
 constexpr int kScanThreads = 1024;
 constexpr int kScanPer = 8;
+constexpr int kSegTilesLog2 = 13;  // 1024 * 8 tiles per segment
+constexpr int kSegBlocksLog2 = kSegTilesLog2 + 6;
 
 __global__ __launch_bounds__(kScanThreads) void rle_scan_tiles_kernel(uint32_t *__restrict__ tiles, long long ntiles,
-                                                                      uint32_t *__restrict__ total_out) {
+                                                                      uint32_t *__restrict__ segs) {
     __shared__ uint32_t wsum[kScanThreads / 64];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const long long chunk = (long long)kScanThreads * kScanPer;
-    auto load = [&](long long c0, uint32_t (&v)[kScanPer]) {
+    const long long c0 = (long long)blockIdx.x << kSegTilesLog2;
+    const long long i0 = c0 + (long long)tid * kScanPer;
+    uint32_t v[kScanPer];
+    if (i0 + kScanPer <= ntiles) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(tiles + i0), b = *reinterpret_cast<const uint4 *>(tiles + i0 + 4);
+        v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+    } else {
 #pragma unroll
-        for (int i = 0; i < kScanPer; ++i) {
-            const long long idx = c0 + (long long)tid * kScanPer + i;
-            v[i] = idx < ntiles ? tiles[idx] : 0u;
-        }
-    };
-    uint32_t carry = 0, nxt[kScanPer];
-    load(0, nxt);
-    for (long long c0 = 0; c0 < ntiles; c0 += chunk) {
-        uint32_t v[kScanPer];
-#pragma unroll
-        for (int i = 0; i < kScanPer; ++i) v[i] = nxt[i];
-        if (c0 + chunk < ntiles) load(c0 + chunk, nxt);
-        uint32_t s = 0;
-#pragma unroll
-        for (int i = 0; i < kScanPer; ++i) s += v[i];
-        const uint32_t inc = wave_inclusive_scan(s);
-        if (lane == 63) wsum[wv] = inc;
-        __syncthreads();
-        uint32_t wpre = 0, ctot = 0;
-#pragma unroll
-        for (int w = 0; w < kScanThreads / 64; ++w) {
-            const uint32_t x = wsum[w];
-            wpre += w < wv ? x : 0u;
-            ctot += x;
-        }
-        __syncthreads();  // wsum is rewritten by the next chunk
-        uint32_t acc = carry + wpre + inc - s;
-#pragma unroll
-        for (int i = 0; i < kScanPer; ++i) {
-            const long long idx = c0 + (long long)tid * kScanPer + i;
-            if (idx < ntiles) tiles[idx] = acc;
-            acc += v[i];
-        }
-        carry += ctot;
+        for (int i = 0; i < kScanPer; ++i) v[i] = i0 + i < ntiles ? tiles[i0 + i] : 0u;
     }
-    if (tid == 0) *total_out = carry;
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) s += v[i];
+    const uint32_t inc = wave_inclusive_scan(s);
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t wpre = 0, ctot = 0;
+#pragma unroll
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        const uint32_t x = wsum[w];
+        wpre += w < wv ? x : 0u;
+        ctot += x;
+    }
+    uint32_t acc = wpre + inc - s;
+    uint32_t out[kScanPer];
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        out[i] = acc;
+        acc += v[i];
+    }
+    if (i0 + kScanPer <= ntiles) {
+        *reinterpret_cast<uint4 *>(tiles + i0) = make_uint4(out[0], out[1], out[2], out[3]);
+        *reinterpret_cast<uint4 *>(tiles + i0 + 4) = make_uint4(out[4], out[5], out[6], out[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanPer; ++i)
+            if (i0 + i < ntiles) tiles[i0 + i] = out[i];
+    }
+    if (tid == 0) segs[blockIdx.x] = ctot;
 }
 
+// offsets[b] += tile prefix (within its segment) + the segment's prefix; the
+// workgroup's segment is uniform, its prefix a wave reduction over <= 128 sums.
 __global__ __launch_bounds__(kRleThreads) void rle_fixup_kernel(uint32_t *__restrict__ offsets,
-                                                                const uint32_t *__restrict__ tiles, long long nblk) {
+                                                                const uint32_t *__restrict__ tiles,
+                                                                const uint32_t *__restrict__ segs, int nsegs,
+                                                                long long nblk) {
+    const int lane = threadIdx.x & 63;
     const long long b = (long long)blockIdx.x * kRleThreads + threadIdx.x;
-    if (b < nblk) offsets[b] += tiles[b >> 6];
+    const int sb = (int)(((long long)blockIdx.x * kRleThreads) >> kSegBlocksLog2);
+    uint32_t p = (lane < sb ? segs[lane] : 0u) + (lane + 64 < sb ? segs[lane + 64] : 0u);
+    p = __builtin_amdgcn_readlane(wave_inclusive_scan(p), 63);
+    if (b < nblk) offsets[b] += tiles[b >> 6] + p;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {  // grand total
+        uint32_t t = (lane < nsegs ? segs[lane] : 0u) + (lane + 64 < nsegs ? segs[lane + 64] : 0u);
+        t = __builtin_amdgcn_readlane(wave_inclusive_scan(t), 63);
+        if (lane == 0) offsets[nblk] = t;
+    }
 }
 
-// ---- emit: one wave per 64-block tile; lane i holds zigzag element i of the
-// current block.  Blocks are processed in groups of kEmitGroup whose 2-byte
-// gathers (one 128-B line per block) are issued one group ahead, across tile
-// boundaries too, so a wave always has a group of loads in flight while it
-// emits the previous one.  Offsets arrive per tile with one coalesced load and
-// are read per block with readlane.  All loads are VMEM (ordered against the
-// symbol stores' data reads), so no store-data hazard arises.
-constexpr int kEmitGroup = 16;
-constexpr int kGroup = 8;  // decode: blocks per group
-
+// ---- emit: one wave per 64-block tile, lane i = zigzag element i of the
+// current block.
+//
+// Address throughput, not bytes, bounded the first versions: a CU's texture
+// addresser takes ~2 lane-addresses per cycle (measured: 2-byte gathers + 4-byte
+// symbol stores ran at 2.1-2.2 lane-addresses/cycle for dense and sparse
+// symbol streams alike).  So the tile's 8 KiB comes in with eight 1 KiB loads
+// (8 lane-addresses per block instead of 64), goes to LDS, and each block's
+// zigzag element per lane is an LDS read.  All 64 LDS reads of a tile happen
+// before its first symbol store, after a vmcnt(0) at the top of the tile that
+// retires the previous tile's stores (store-data hazard); the next
+// tile's loads are in flight meanwhile.  Per block (~14 VALU): E = ballot(emit);
+// the symbol's index is mbcnt(E); its run is lane - 63 + clz64(((E << 1) | 1) &
+// lanes <= i), the sentinel bit 0 standing for "no earlier symbol".  Stores are
+// unconditional: lanes with nothing to store aim past num_records.
 __device__ __forceinline__ int tile_blocks(long long t, long long nblk) {
     const long long r = nblk - t * 64;
-    return r < 64 ? (int)r : 64;
+    return r < 0 ? 0 : r < 64 ? (int)r : 64;
 }
 
-__device__ __forceinline__ void emit_gather(const int16_t *coef, long long t, int g, int nb, int nat,
-                                            int16_t (&v)[kEmitGroup]) {
-    const int16_t *base = coef + t * 64 * 64 + nat;
-#pragma unroll
-    for (int u = 0; u < kEmitGroup; ++u) {
-        const int jb = g + u < nb ? g + u : nb - 1;
-        v[u] = base[(long long)jb * 64];
-    }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const int16_t *coef, long long t, int nb) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t *>(coef) + (nb ? t * 64 * 64 : 0), (short)0, nb * 128,
+                                             0x00020000);
 }
 
-__global__ __launch_bounds__(kRleThreads) void rle_emit_kernel(const int16_t *__restrict__ coef, long long nblk,
+typedef uint32_t u4r __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                const uint32_t *__restrict__ offsets,
                                                                uint32_t *__restrict__ symbols, long long ntiles) {
-    const int lane = threadIdx.x & 63;
+    __shared__ u4r tiles_lds[kRleWaves][64 * 8];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long stride = (long long)gridDim.x * kRleWaves;
-    const int nat = kZigzag[lane];
-    const uint64_t below = lane_mask_below(lane);
-    long long t = (long long)blockIdx.x * kRleWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t zoff = 2u * kZigzag[lane];
+    const uint64_t upto = ~0ull >> (63 - lane);  // lanes 0..lane
+    const uint32_t upto_lo = (uint32_t)upto, upto_hi = (uint32_t)(upto >> 32);
+    const __amdgpu_buffer_rsrc_t roff = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t *>(offsets), (short)0, (int)(nblk * 4 < 0x7FFFFFFF ? nblk * 4 : 0x7FFFFFFF), 0x00020000);
+    long long t = (long long)blockIdx.x * kRleWaves + wv;
     if (t >= ntiles) return;
-    int g = 0, nb = tile_blocks(t, nblk);
-    uint32_t offv = offsets[t * 64 + (lane < nb ? lane : nb - 1)];
-    int16_t v[kEmitGroup];
-    emit_gather(coef, t, 0, nb, nat, v);
-    for (;;) {
-        // the next group (possibly the first of the wave's next tile), requested before this one is emitted
-        long long tn = t;
-        int gn = g + kEmitGroup, nbn = nb;
-        if (gn >= nb) {
-            tn = t + stride;
-            gn = 0;
-            nbn = tn < ntiles ? tile_blocks(tn, nblk) : 1;
-        }
-        int16_t vn[kEmitGroup];
-        uint32_t offn = offv;
-        if (tn < ntiles) {
-            emit_gather(coef, tn, gn, nbn, nat, vn);
-            if (gn == 0) offn = offsets[tn * 64 + (lane < nbn ? lane : nbn - 1)];
-        }
+    u4r nq[8];
+    uint32_t noff;
+    auto load_tile = [&](long long tt) {  // past the last tile: everything clipped, no traffic
+        const __amdgpu_buffer_rsrc_t rs = tile_rsrc(coef, tt, tile_blocks(tt, nblk));
 #pragma unroll
-        for (int u = 0; u < kEmitGroup; ++u) {
-            if (g + u >= nb) break;
-            const uint32_t o = __builtin_amdgcn_readlane(offv, g + u);
-            const bool emit = v[u] != 0 || lane == 63;
-            const uint64_t prev = __builtin_amdgcn_ballot_w64(emit) & below;
-            const int p = prev ? 63 - __builtin_clzll(prev) : -1;
-            const uint32_t runlen = (uint32_t)(lane - p - 1) + (lane == 63 && v[u] == 0 ? 1u : 0u);
-            if (emit) symbols[o + (uint32_t)__builtin_popcountll(prev)] = (uint32_t)(uint16_t)v[u] | (runlen << 16);
-        }
-        if (tn >= ntiles) break;
-        t = tn;
-        g = gn;
-        nb = nbn;
-        offv = offn;
+        for (int k = 0; k < 8; ++k) nq[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, 2 /* nt */);
+        noff = __builtin_amdgcn_raw_buffer_load_b32(roff, tt < ntiles ? (uint32_t)(tt * 64 + lane) * 4u : 0xFFFFFFF0u,
+                                                    0, 0);
+    };
+    load_tile(t);
+    char *lt = reinterpret_cast<char *>(tiles_lds[wv]);
+    for (; t < ntiles; t += stride) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this tile's loads and the previous tile's stores
+        const uint32_t offv = noff;
 #pragma unroll
-        for (int u = 0; u < kEmitGroup; ++u) v[u] = vn[u];
+        for (int k = 0; k < 8; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = nq[k];  // the tile's 8 KiB, in order
+        load_tile(t + stride);
+        wave_sync_lds();
+        uint32_t z[32];  // two blocks' elements per register (64 live VGPRs would halve the occupancy)
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+            z[u] = (uint32_t)*reinterpret_cast<const uint16_t *>(lt + 2 * u * 128 + zoff) |
+                   ((uint32_t)*reinterpret_cast<const uint16_t *>(lt + (2 * u + 1) * 128 + zoff) << 16);
+        const int nb = tile_blocks(t, nblk);
+        // the tile's symbols start at offsets[64t]: a per-tile descriptor keeps the
+        // 32-bit voffset small (the stream itself may exceed 4 GiB)
+        const uint32_t o0 = __builtin_amdgcn_readlane(offv, 0);
+        const __amdgpu_buffer_rsrc_t rsym =
+            __builtin_amdgcn_make_buffer_rsrc(symbols + o0, (short)0, 64 * 64 * 4, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < 64; ++u) {
+            const uint32_t val = (u & 1) ? z[u >> 1] >> 16 : z[u >> 1] & 0xFFFFu;
+            const bool emit = val != 0u || lane == 63;
+            const uint64_t E = __builtin_amdgcn_ballot_w64(emit);
+            const uint64_t E2 = (E << 1) | 1ull;  // SALU; bit 0: "no earlier symbol"
+            const uint64_t prev =
+                (uint64_t)(upto_lo & (uint32_t)E2) | ((uint64_t)(upto_hi & (uint32_t)(E2 >> 32)) << 32);
+            uint32_t runlen = (uint32_t)(lane - 63 + __builtin_clzll(prev));
+            if (lane == 63 && val == 0u) runlen += 1u;  // the last symbol's run counts itself (src/entropy.c:231-233)
+            const uint32_t idx =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(E >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)E, 0u));
+            const uint32_t o = __builtin_amdgcn_readlane(offv, u);
+            const uint32_t addr = (emit && u < nb) ? (o - o0 + idx) * 4u : 0xFFFFFFF0u;  // dropped past num_records
+            __builtin_amdgcn_raw_buffer_store_b32(val | (runlen << 16), rsym, addr, 0, 0);
+        }
     }
 }
 
-// ---- decode: one wave per 64-block tile, groups of 8 blocks: the symbol loads
-// of a group are in flight together (each block's range from readlane of the
-// tile's coalesced offsets); each block is rebuilt in the wave's 64-entry LDS
-// row (zeroed, symbols scattered to their zigzag positions -- LDS writes of one
-// wave are performed in order), read back in natural order, and the group's 8
-// blocks are stored as 128-B rows.
-//
-// LDS loads and the store-data race (fdct8.hip v2 / DESIGN.md): the previous
-// group's stores may still be reading their data VGPRs when this group's LDS
-// reads return, so those 8 registers are kept live across the reads (the LDS
-// reads cannot land in them); the stores' address operands are loop-invariant
-// (voff) or scalar.
+// ---- decode: one wave per 64-block tile, rebuilt 32 blocks at a time in a
+// natural-order LDS copy (4 KiB per wave: 8 waves/SIMD) and written as 1 KiB
+// stores (8 lane-addresses per block).  Per block: its symbols (lane s = symbol
+// s, one load; the next group's loads are issued before this group is
+// scattered), an inclusive scan of run+1 gives each symbol's zigzag position
+// (run_length_decode: pos += run; zigzag[pos++] = value, dropped past the end,
+// src/entropy.c:327-351), and the value is scattered to its natural index
+// (zigzag_to_block, :183-210, through an LDS copy of the order).  Each half
+// tile's LDS work starts after a vmcnt(0) that retires the previous half's
+// stores (store-data hazard); no store is issued inside the half.
+constexpr int kHalf = 32;
+
+__device__ __forceinline__ void decode_loads(const uint32_t *symbols, uint32_t offv, int g, int nb, int lane,
+                                             uint32_t (&sy)[kGroup], uint32_t (&cnt)[kGroup]) {
+#pragma unroll
+    for (int u = 0; u < kGroup; ++u) {
+        const int jb = g + u < nb ? g + u : nb - 1;
+        const uint32_t o0 = __builtin_amdgcn_readlane(offv, jb), o1 = __builtin_amdgcn_readlane(offv, jb + 1);
+        cnt[u] = g + u < nb ? o1 - o0 : 0u;
+        sy[u] = (uint32_t)lane < cnt[u] ? symbols[o0 + lane] : 0u;
+    }
+}
+
 __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t *__restrict__ symbols,
                                                                  const uint32_t *__restrict__ offsets, long long nblk,
                                                                  int16_t *__restrict__ coef, long long ntiles) {
-    __shared__ int16_t row[kRleWaves][64];
+    __shared__ u4r half_lds[kRleWaves][kHalf * 8];
+    __shared__ uint8_t zz[64];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (threadIdx.x < 64) zz[threadIdx.x] = kZigzag[threadIdx.x];
+    __syncthreads();
     const long long stride = (long long)gridDim.x * kRleWaves;
-    const int zpos = kUnzigzag[lane];
-    uint32_t voff = (uint32_t)lane * 2u;
-    uint32_t outv[kGroup];
-#pragma unroll
-    for (int u = 0; u < kGroup; ++u) outv[u] = 0;
+    char *lt = reinterpret_cast<char *>(half_lds[wv]);
     for (long long t = (long long)blockIdx.x * kRleWaves + wv; t < ntiles; t += stride) {
         const long long b0 = t * 64;
-        const int nb = nblk - b0 < 64 ? (int)(nblk - b0) : 64;
+        const int nb = tile_blocks(t, nblk);
         const uint32_t offv = offsets[b0 + (lane < nb ? lane : nb)];  // lane nb: the end of the tile
-        for (int g = 0; g < nb; g += kGroup) {
+        for (int h = 0; h < nb; h += kHalf) {
+            const int he = nb < h + kHalf ? nb : h + kHalf;
             uint32_t sy[kGroup], cnt[kGroup];
+            decode_loads(symbols, offv, h, nb, lane, sy, cnt);
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the previous half's stores, before any LDS read
 #pragma unroll
-            for (int u = 0; u < kGroup; ++u) {
-                const int jb = g + u < nb ? g + u : nb - 1;
-                const uint32_t o0 = __builtin_amdgcn_readlane(offv, jb), o1 = __builtin_amdgcn_readlane(offv, jb + 1);
-                cnt[u] = g + u < nb ? o1 - o0 : 0u;
-                sy[u] = (uint32_t)lane < cnt[u] ? symbols[o0 + lane] : 0u;
-            }
+            for (int k = 0; k < 4; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
+            for (int g = h; g < he; g += kGroup) {
+                uint32_t nsy[kGroup], ncnt[kGroup];
+                decode_loads(symbols, offv, g + kGroup < he ? g + kGroup : g, nb, lane, nsy, ncnt);
 #pragma unroll
-            for (int u = 0; u < kGroup; ++u) asm volatile("" : "+v"(outv[u]));
-            uint32_t val[kGroup];
+                for (int u = 0; u < kGroup; ++u) {
+                    const uint32_t e = wave_inclusive_scan((uint32_t)lane < cnt[u] ? (sy[u] >> 16) + 1u : 0u);
+                    const uint32_t pos = e - 1u;
+                    if ((uint32_t)lane < cnt[u] && pos < 64u && g + u < he)
+                        *reinterpret_cast<int16_t *>(lt + (g - h + u) * 128 + 2 * zz[pos]) = (int16_t)(sy[u] & 0xFFFFu);
+                }
 #pragma unroll
-            for (int u = 0; u < kGroup; ++u) {
-                const uint32_t e = wave_inclusive_scan((uint32_t)lane < cnt[u] ? (sy[u] >> 16) + 1u : 0u);
-                row[wv][lane] = 0;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint32_t pos = e - 1u;  // run_length_decode: pos += run; zigzag[pos++] = value (dropped past the end)
-                if ((uint32_t)lane < cnt[u] && pos < 64u) row[wv][pos] = (int16_t)(sy[u] & 0xFFFFu);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                val[u] = (uint32_t)(uint16_t)row[wv][zpos];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-#pragma unroll
-            for (int u = 0; u < kGroup; ++u) asm volatile("" ::"v"(outv[u]));
-#pragma unroll
-            for (int u = 0; u < kGroup; ++u) {
-                outv[u] = val[u];
-                if (g + u < nb) {
-                    const __amdgpu_buffer_rsrc_t rs =
-                        __builtin_amdgcn_make_buffer_rsrc(coef + (b0 + g + u) * 64, (short)0, 128, 0x00020000);
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)outv[u], rs, voff, 0, 0);
+                for (int u = 0; u < kGroup; ++u) {
+                    sy[u] = nsy[u];
+                    cnt[u] = ncnt[u];
                 }
             }
-            asm volatile("" : "+v"(voff));
+            wave_sync_lds();
+            u4r val[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) val[k] = reinterpret_cast<const u4r *>(lt)[k * 64 + lane];
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(coef + (b0 + h) * 64, (short)0, (he - h) * 128, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, 2);
         }
     }
 }
@@ -303,17 +341,23 @@ static unsigned grid_for(long long waves_wanted, int num_cus) {
     return (unsigned)(g < 1 ? 1 : g > cap ? cap : g);
 }
 
-size_t rle_workspace_bytes(long long nblk) { return (size_t)((nblk + 63) / 64) * sizeof(uint32_t); }
+// tile totals, then (16-B aligned) the segment sums
+size_t rle_workspace_bytes(long long nblk) {
+    const long long ntiles = (nblk + 63) / 64;
+    return (size_t)((ntiles + 3) / 4 * 4) * 4 + 128 * 4;
+}
 
 hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offsets, void *ws, hipStream_t stream,
                             int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
+    const int nsegs = (int)((ntiles + (1 << kSegTilesLog2) - 1) >> kSegTilesLog2);  // <= 128 for nblk < 2^26
     uint32_t *tiles = (uint32_t *)ws;
+    uint32_t *segs = tiles + (ntiles + 3) / 4 * 4;
     hipLaunchKernelGGL(rle_count_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, coef, nblk,
                        offsets, tiles, ntiles);
-    hipLaunchKernelGGL(rle_scan_tiles_kernel, dim3(1), dim3(kScanThreads), 0, stream, tiles, ntiles, offsets + nblk);
+    hipLaunchKernelGGL(rle_scan_tiles_kernel, dim3(nsegs), dim3(kScanThreads), 0, stream, tiles, ntiles, segs);
     hipLaunchKernelGGL(rle_fixup_kernel, dim3((unsigned)((nblk + kRleThreads - 1) / kRleThreads)), dim3(kRleThreads),
-                       0, stream, offsets, (const uint32_t *)tiles, nblk);
+                       0, stream, offsets, (const uint32_t *)tiles, (const uint32_t *)segs, nsegs, nblk);
     return hipGetLastError();
 }
 

@@ -45,6 +45,7 @@ for step in "$@"; do
     ceil3) run ceil3 120 tools/ubench/stream_ceiling3 ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
+    profaux) run profaux 600 rocprofv3 --kernel-trace --stats -d $OUT/profaux -o run --output-format csv -- python tools/aux_bench.py ;;
     rtb) run rtb 300 bash -c "python tools/rt_bench.py 64 && python tools/rt_bench.py 64 --adaptive" ;;
     testrt) run pytest_rt 600 python -m pytest tests -m gpu -x -q -k "round_trip or planes" ;;
     pmcq1) run pmcq1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_q1 -o run --output-format csv -- python tools/ab_bench.py --variants 2 --rounds 3 ;;
