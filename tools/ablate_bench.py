@@ -24,6 +24,8 @@ for m, name in sorted(NAMES.items()):
 import glob  # noqa: E402
 for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libpolicy_*.so"))):  # tools/ubench/policy.sh
     libs["policy-" + os.path.basename(p)[len("libpolicy_"):-3]] = p
+for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libvar_*.so"))):  # tools/ubench/variant.sh
+    libs["var-" + os.path.basename(p)[len("libvar_"):-3]] = p
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 px = dct_amd.synth(7, "uniform", 3840, 2160, F)
 d = dct_amd.plane_desc(px)
@@ -48,6 +50,17 @@ for r in range(12):
         torch.cuda.synchronize()
         if r >= 2:
             times[name].append(e0.elapsed_time(e1) * 1e-3)
+# variants that must be correct: compare with the default build
+ref = None
+for name, (L, h) in plans.items():
+    if name == "full" or name.startswith("policy-") or name.startswith("var-"):
+        o = torch.zeros_like(out)
+        assert L.dctq_forward_quant(h, C.byref(d), C.c_void_p(o.data_ptr()), None, stream) == 0
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = o
+        elif not torch.equal(o, ref):
+            print(f"{name}: OUTPUT DIFFERS from the default build ({int((o != ref).sum())} coefficients)")
 for name, ts in times.items():
     med = statistics.median(ts)
     print(f"{name:24s} median {med*1e6:7.1f} us  {nblk*192/med/1e9:6.0f} GB/s")
