@@ -78,6 +78,13 @@ struct PlaneSet {
     int n;
 };
 
+// The encoder's planes: PlaneSet (coef/var unused) plus each plane's first block
+// in the concatenated block numbering of the offsets array; blk_first[n] = total.
+struct EncodeSet {
+    PlaneSet ps;
+    uint32_t blk_first[kMaxPlanes + 1];
+};
+
 // The fused round trip's planes: forward outputs as PlaneSet, plus fp32 recon per plane.
 struct RoundTripSet {
     PlaneSet ps;
@@ -91,11 +98,18 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
 size_t fdct8_ring_bytes(int workgroups);
 hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
                             hipStream_t stream, int num_cus);
+size_t encode_workspace_bytes(long long nbatch);
+hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *offsets,
+                         uint32_t *symbols, unsigned long long capacity, void *ws, hipStream_t stream, int num_cus);
 hipError_t launch_fdct8_float_pair(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream,
                                    int num_cus);
 hipError_t launch_idct8_pair(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
                              long long nblk, float *recon, hipStream_t stream, int num_cus);
 size_t rle_workspace_bytes(long long nblk);
+size_t rle_scan_workspace_bytes(long long ntiles);
+hipError_t launch_rle_scan(void *ws, long long ntiles, hipStream_t stream);
+hipError_t launch_rle_fixup(uint32_t *offsets, long long nblk, const void *ws, long long ntiles, long long tile0,
+                            uint32_t *total_out, hipStream_t stream);
 hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offsets, void *ws, hipStream_t stream,
                             int num_cus);
 hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,

@@ -320,4 +320,66 @@ __device__ __forceinline__ int pop_flag(uint32_t &mlo, uint32_t &mhi) {
     return (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
 }
 
+// The forward of one 64-block batch with every flagged coefficient resolved IN
+// PLACE (for consumers that read the final ints from the stage in the same
+// launch: the fused round trip and the encoder): fdct8_compute into the stage,
+// the constant-block DC table, then each owning lane recomputes its flagged
+// coefficients in the reference's exact order from the pixels still in its
+// registers.  Returns the number of exact recomputations of this lane.
+template <bool ADAPTIVE, bool VAR>
+__device__ __forceinline__ uint32_t forward_exact_batch(const DevTables *__restrict__ dev, const uint2 (&cur)[8],
+                                                        uint4 *stage, int lane, int wv, bool valid,
+                                                        int32_t &var_num) {
+    uint32_t mlo, mhi;
+    fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
+    flat_dc_fix(dev, cur, stage, lane, wv, mlo);
+    if (!valid) mlo = mhi = 0;
+    uint32_t n = 0;
+    if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) {
+        int16_t *mine16 = reinterpret_cast<int16_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 2);
+        while (mlo | mhi) {
+            const int c = pop_flag(mlo, mhi);
+            // opaque copy: hoisted out of this loop, the 64 fp64 pixel conversions
+            // would be 128 live VGPRs (and spill the whole kernel)
+            uint2 rows[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                rows[r] = cur[r];
+                asm volatile("" : "+v"(rows[r].x), "+v"(rows[r].y));
+            }
+            mine16[c] = (int16_t)exact_from_rows<ADAPTIVE>(rows, c, dev);
+            ++n;
+        }
+    }
+    return n;
+}
+
+// The wave's stage as the 8 chunks of 1 KiB stores: chunk c, lane l = 16 B at
+// byte 16 (64c + l) of the batch's 8 KiB (block (64c + l) / 8).
+__device__ __forceinline__ void stage_chunks(const uint4 *stage, int wv, int lane, u4v (&val)[8]) {
+    const uint2 *st64 = reinterpret_cast<const uint2 *>(stage) + wv * 64 * (kPitch2 / 8);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const int m = c * 64 + lane;
+        const int bl = m >> 3;
+        const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
+        val[c] = u4v{lo.x, lo.y, hi.x, hi.y};
+    }
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// vmcnt(0): the wave's stores have read their data VGPRs (and left the CU).
+__device__ __forceinline__ void retire_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// Rows of global batch gn (past the end: the last plane's block 0, unused).
+__device__ __forceinline__ void prefetch_batch(const PlaneSet &ps, uint32_t gn, int lane, uint2 (&nxt)[8]) {
+    const int kn = plane_of(ps, gn);
+    load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
+}
+
 }  // namespace dctq

@@ -18,19 +18,9 @@
 //   dctq_rle_decode: run_length_decode (:327-351) + zigzag_to_block (:183-210),
 //                    one wave per tile through a 64-entry LDS row.
 #include "scan_core.h"
+#include "zigzag.h"
 
 namespace dctq {
-
-// zigzag position k -> natural index (src/entropy.c:158-178 for n = 8)
-__constant__ uint8_t kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
-                                    12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
-                                    35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
-                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-// natural index -> zigzag position
-__constant__ uint8_t kUnzigzag[64] = {0,  1,  5,  6,  14, 15, 27, 28, 2,  4,  7,  13, 16, 26, 29, 42,
-                                      3,  8,  12, 17, 25, 30, 41, 43, 9,  11, 18, 24, 31, 40, 44, 53,
-                                      10, 19, 23, 32, 39, 45, 52, 54, 20, 22, 33, 38, 46, 51, 55, 60,
-                                      21, 34, 37, 47, 50, 56, 59, 61, 35, 36, 48, 49, 57, 58, 62, 63};
 
 constexpr int kRleWaves = 4;
 constexpr int kRleThreads = 64 * kRleWaves;
@@ -150,23 +140,32 @@ __global__ __launch_bounds__(kScanThreads) void rle_scan_tiles_kernel(uint32_t *
     if (tid == 0) segs[blockIdx.x] = ctot;
 }
 
-// offsets[b] += tile prefix (within its segment) + the segment's prefix; the
-// workgroup's segment is uniform, its prefix a wave reduction over <= 128 sums.
+// offsets[b] += tile prefix (within its segment) + the segment's prefix, for
+// blocks b of one plane whose tiles start at global tile tile0 (0 for a plain
+// coefficient array; the encoder runs one fix-up per plane).  The <= 128 segment
+// sums are scanned into LDS by the first wave; total_out (if set) gets the
+// grand total.
 __global__ __launch_bounds__(kRleThreads) void rle_fixup_kernel(uint32_t *__restrict__ offsets,
                                                                 const uint32_t *__restrict__ tiles,
                                                                 const uint32_t *__restrict__ segs, int nsegs,
-                                                                long long nblk) {
+                                                                long long nblk, long long tile0,
+                                                                uint32_t *__restrict__ total_out) {
+    __shared__ uint32_t segpre[129];
     const int lane = threadIdx.x & 63;
-    const long long b = (long long)blockIdx.x * kRleThreads + threadIdx.x;
-    const int sb = (int)(((long long)blockIdx.x * kRleThreads) >> kSegBlocksLog2);
-    uint32_t p = (lane < sb ? segs[lane] : 0u) + (lane + 64 < sb ? segs[lane + 64] : 0u);
-    p = __builtin_amdgcn_readlane(wave_inclusive_scan(p), 63);
-    if (b < nblk) offsets[b] += tiles[b >> 6] + p;
-    if (blockIdx.x == 0 && threadIdx.x < 64) {  // grand total
-        uint32_t t = (lane < nsegs ? segs[lane] : 0u) + (lane + 64 < nsegs ? segs[lane + 64] : 0u);
-        t = __builtin_amdgcn_readlane(wave_inclusive_scan(t), 63);
-        if (lane == 0) offsets[nblk] = t;
+    if (threadIdx.x < 64) {  // exclusive prefix of the segment sums, two per lane
+        const uint32_t a = 2 * lane < nsegs ? segs[2 * lane] : 0u, b = 2 * lane + 1 < nsegs ? segs[2 * lane + 1] : 0u;
+        const uint32_t inc = wave_inclusive_scan(a + b);
+        segpre[2 * lane] = inc - a - b;
+        segpre[2 * lane + 1] = inc - b;
+        if (lane == 63) segpre[128] = inc;
     }
+    __syncthreads();
+    const long long b = (long long)blockIdx.x * kRleThreads + threadIdx.x;
+    if (b < nblk) {
+        const long long t = tile0 + (b >> 6);
+        offsets[b] += tiles[t] + segpre[t >> kSegTilesLog2];
+    }
+    if (total_out && blockIdx.x == 0 && threadIdx.x == 0) *total_out = segpre[128];
 }
 
 // ---- emit: one wave per 64-block tile, lane i = zigzag element i of the
@@ -342,23 +341,36 @@ static unsigned grid_for(long long waves_wanted, int num_cus) {
 }
 
 // tile totals, then (16-B aligned) the segment sums
-size_t rle_workspace_bytes(long long nblk) {
-    const long long ntiles = (nblk + 63) / 64;
-    return (size_t)((ntiles + 3) / 4 * 4) * 4 + 128 * 4;
+size_t rle_scan_workspace_bytes(long long ntiles) { return (size_t)((ntiles + 3) / 4 * 4) * 4 + 128 * 4; }
+size_t rle_workspace_bytes(long long nblk) { return rle_scan_workspace_bytes((nblk + 63) / 64); }
+
+// Scan of ntiles tile totals in ws (in place, by segment); then per plane
+// launch_rle_fixup.
+hipError_t launch_rle_scan(void *ws, long long ntiles, hipStream_t stream) {
+    const int nsegs = (int)((ntiles + (1 << kSegTilesLog2) - 1) >> kSegTilesLog2);  // <= 128 for < 2^26 blocks
+    uint32_t *tiles = (uint32_t *)ws;
+    hipLaunchKernelGGL(rle_scan_tiles_kernel, dim3(nsegs), dim3(kScanThreads), 0, stream, tiles, ntiles,
+                       tiles + (ntiles + 3) / 4 * 4);
+    return hipGetLastError();
+}
+
+hipError_t launch_rle_fixup(uint32_t *offsets, long long nblk, const void *ws, long long ntiles, long long tile0,
+                            uint32_t *total_out, hipStream_t stream) {
+    const int nsegs = (int)((ntiles + (1 << kSegTilesLog2) - 1) >> kSegTilesLog2);
+    const uint32_t *tiles = (const uint32_t *)ws;
+    hipLaunchKernelGGL(rle_fixup_kernel, dim3((unsigned)((nblk + kRleThreads - 1) / kRleThreads)), dim3(kRleThreads),
+                       0, stream, offsets, tiles, tiles + (ntiles + 3) / 4 * 4, nsegs, nblk, tile0, total_out);
+    return hipGetLastError();
 }
 
 hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offsets, void *ws, hipStream_t stream,
                             int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
-    const int nsegs = (int)((ntiles + (1 << kSegTilesLog2) - 1) >> kSegTilesLog2);  // <= 128 for nblk < 2^26
-    uint32_t *tiles = (uint32_t *)ws;
-    uint32_t *segs = tiles + (ntiles + 3) / 4 * 4;
     hipLaunchKernelGGL(rle_count_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, coef, nblk,
-                       offsets, tiles, ntiles);
-    hipLaunchKernelGGL(rle_scan_tiles_kernel, dim3(nsegs), dim3(kScanThreads), 0, stream, tiles, ntiles, segs);
-    hipLaunchKernelGGL(rle_fixup_kernel, dim3((unsigned)((nblk + kRleThreads - 1) / kRleThreads)), dim3(kRleThreads),
-                       0, stream, offsets, (const uint32_t *)tiles, (const uint32_t *)segs, nsegs, nblk);
-    return hipGetLastError();
+                       offsets, (uint32_t *)ws, ntiles);
+    hipError_t e = launch_rle_scan(ws, ntiles, stream);
+    if (e != hipSuccess) return e;
+    return launch_rle_fixup(offsets, nblk, ws, ntiles, 0, offsets + nblk, stream);
 }
 
 hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,

@@ -33,20 +33,8 @@ namespace dctq {
 #ifndef DCTQ_RT_OCC
 #define DCTQ_RT_OCC 4  // waves per SIMD (launch bound)
 #endif
-#ifndef DCTQ_RT_NOEXACT
-#define DCTQ_RT_NOEXACT 0  // diagnostic only: skip the exact recomputation of tie coefficients
-#endif
 
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
-
-// vmcnt(0): the wave's stores have read their data VGPRs (and left the CU).
-__device__ __forceinline__ void retire_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // Dequantize + inverse DCT + 128 of one 32-block sub-batch, lane (h, j) holding
 // rows 4h..4h+3 of block j (8 int16 per uint4) and the block's var_num; fp32
@@ -102,12 +90,6 @@ __device__ __forceinline__ void inverse_half(const DevTables *__restrict__ dev, 
     }
 }
 
-// Rows of global batch gn (past the end: the last plane's block 0, unused).
-__device__ __forceinline__ void prefetch(const PlaneSet &ps, uint32_t gn, int lane, uint2 (&nxt)[8]) {
-    const int kn = plane_of(ps, gn);
-    load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
-}
-
 template <bool ADAPTIVE, bool VAR, bool STATS>
 __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet rt, const DevTables *__restrict__ dev,
                                                           unsigned long long *fallbacks) {
@@ -119,7 +101,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
     const uint32_t step = gridDim.x * kWaves;
     uint32_t g = blockIdx.x * kWaves + wv;
     uint2 nxt[8];
-    prefetch(ps, g, lane, nxt);
+    prefetch_batch(ps, g, lane, nxt);
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
     uint32_t exact_count = 0;
@@ -132,45 +114,21 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        if (DCTQ_RT_EARLY_PREFETCH) prefetch(ps, g + step, lane, nxt);
+        if (DCTQ_RT_EARLY_PREFETCH) prefetch_batch(ps, g + step, lane, nxt);
 
         // ---- 1. forward into the stage; ties resolved in place
-        uint32_t mlo, mhi;
         int32_t var_num;
-        fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
-        flat_dc_fix(dev, cur, stage, lane, wv, mlo);
-        if (!valid) mlo = mhi = 0;
-        if (!DCTQ_RT_NOEXACT && __builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) {
-            int16_t *mine16 = reinterpret_cast<int16_t *>(wstage + lane * kPitch2);
-            while (mlo | mhi) {
-                const int c = pop_flag(mlo, mhi);
-                // opaque copy: hoisted out of this loop, the 64 fp64 pixel
-                // conversions would be 128 live VGPRs (and spill the whole kernel)
-                uint2 rows[8];
-#pragma unroll
-                for (int r = 0; r < 8; ++r) {
-                    rows[r] = cur[r];
-                    asm volatile("" : "+v"(rows[r].x), "+v"(rows[r].y));
-                }
-                mine16[c] = (int16_t)exact_from_rows<ADAPTIVE>(rows, c, dev);
-                if (STATS) ++exact_count;
-            }
-        }
+        const uint32_t ne = forward_exact_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num);
+        if (STATS) exact_count += ne;
         retire_stores();  // the previous batch's recon stores (long issued) before the read-back
         wave_sync();
 
         // ---- 2. read-back: coefficient chunks + the inverse's half blocks
         const uint32_t left = (uint32_t)p.nblk - b * 64;
         const uint32_t nb = left < 64u ? left : 64u;
-        const uint2 *st64 = reinterpret_cast<const uint2 *>(wstage);
         u4v val[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const int m = c * 64 + lane;
-            const int bl = m >> 3;
-            const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
-            val[c] = u4v{lo.x, lo.y, hi.x, hi.y};
-        }
+        stage_chunks(stage, wv, lane, val);
+        const uint2 *st64 = reinterpret_cast<const uint2 *>(wstage);
         uint4 qa[4], qb[4];
         {
             const uint2 *sa = st64 + j * (kPitch2 / 8) + h * 8;  // block j, rows 4h..4h+3 (64 B)
@@ -204,7 +162,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         retire_stores();
         wave_sync();
         store_stage(stage, wv, lane, recon, (nb < 32u ? nb : 32u) * 256u);
-        if (!DCTQ_RT_EARLY_PREFETCH) prefetch(ps, g + step, lane, nxt);
+        if (!DCTQ_RT_EARLY_PREFETCH) prefetch_batch(ps, g + step, lane, nxt);
         // keep inverse B's inputs packed until here (converted early they are 64 more live VGPRs)
 #pragma unroll
         for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(qb[r].x), "+v"(qb[r].y), "+v"(qb[r].z), "+v"(qb[r].w));

@@ -576,3 +576,45 @@ def test_rle_large_planes(T, dm):
     assert np.array_equal(off.cpu().numpy().view(np.uint32), woff)
     assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym)
     assert np.array_equal(dm.rle_decode(sym, off).cpu().numpy(), c.cpu().numpy())
+
+
+def test_encode_planes_fused(T, dm):
+    """dctq_encode_planes (forward + zigzag/RLE, coefficients never stored) equals the
+    oracle's run_length_encode of the oracle's quantized planes, blocks numbered plane
+    by plane: ragged planes, a frame stack, tie-heavy step blocks (ties resolved before
+    counting: a tie can decide zero vs nonzero), adaptive plans."""
+    import oracle as O
+    rng = np.random.default_rng(44)
+    stack = np.stack([O.synth_plane(90 + f, f % 4, 40, 24) for f in range(3)])
+    sets = [[O.synth_plane(7, 0, 8 * 65, 8 * 9), _step_blocks(rng, 7, 13), O.synth_plane(8, 1, 8, 8), stack],
+            [_step_blocks(rng, 21, 37)], [O.synth_plane(9, 3, 8 * 129, 8 * 3), O.synth_plane(10, 2, 64, 64)]]
+    for q, ad in [(50, 0), (50, 1), (90, 0), (10, 1), (100, 0)]:
+        plan = dm.Plan(q, ad)
+        for planes in sets:
+            want = np.concatenate([np.concatenate([O.forward_plane(f, q, ad) for f in (p if p.ndim == 3 else [p])])
+                                   for p in planes])
+            woff, wsym = O.rle_encode_plane(want)
+            off, sym = plan.encode_planes([gpu_px(T, p) for p in planes])
+            assert np.array_equal(off.cpu().numpy().view(np.uint32), woff), (q, ad)
+            assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), (q, ad)
+
+
+def test_encode_capacity_and_large(T, dm):
+    """Symbols past the capacity are dropped while the offsets stay complete; and a
+    multi-plane encode past one scan segment (5 4K frames + 1080p chroma) equals
+    forward_quant_planes + rle_encode on the GPU."""
+    import oracle as O
+    px = gpu_px(T, O.synth_plane(12, 0, 256, 128))
+    plan = dm.Plan(50, 0)
+    off, sym = plan.encode_planes([px])
+    total = int(off[-1].item())
+    off2, sym2 = plan.encode_planes([px], capacity=total // 3)
+    assert np.array_equal(off.cpu().numpy(), off2.cpu().numpy())
+    assert sym2.numel() == total // 3 and np.array_equal(sym2.cpu().numpy(), sym[:total // 3].cpu().numpy())
+    luma = dm.synth(13, "uniform", 3840, 2160, 5)
+    chroma = dm.synth(14, "smooth", 1920, 1080, 3)
+    off, sym = plan.encode_planes([luma, chroma])
+    coefs = plan.forward_quant_planes([luma, chroma])
+    woff, wsym = dm.rle_encode(T.cat(coefs).contiguous())
+    assert T.equal(off, woff)
+    assert T.equal(sym, wsym)

@@ -45,6 +45,8 @@ for step in "$@"; do
     ceil3) run ceil3 120 tools/ubench/stream_ceiling3 ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
+    enc) run enc 300 python tools/enc_bench.py ;;
+    profenc) run profenc 600 rocprofv3 --kernel-trace --stats -d $OUT/profenc -o run --output-format csv -- python tools/enc_bench.py ;;
     profaux) run profaux 600 rocprofv3 --kernel-trace --stats -d $OUT/profaux -o run --output-format csv -- python tools/aux_bench.py ;;
     rtb) run rtb 300 bash -c "python tools/rt_bench.py 64 && python tools/rt_bench.py 64 --adaptive" ;;
     testrt) run pytest_rt 600 python -m pytest tests -m gpu -x -q -k "round_trip or planes" ;;
