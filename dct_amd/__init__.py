@@ -49,7 +49,7 @@ def lib() -> C.CDLL:
             "dctq_forward_quant_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_round_trip_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, vp], i),
             "dctq_encode_workspace_bytes": ([ll], C.c_size_t),
-            "dctq_encode_planes": ([vp, C.POINTER(_Plane), i, vp, vp, ll, vp, vp], i),
+            "dctq_encode_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, ll, vp, vp], i),
             "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
             "dctq_inverse": ([vp, vp, vp, ll, vp, vp], i),
             "dctq_synth": ([C.c_uint64, i, C.POINTER(_Plane), vp], i),
@@ -170,24 +170,29 @@ class Plan:
                                             C.cast(rp, C.c_void_p), _stream_ptr(stream)))
         return outs, recons
 
-    def encode_planes(self, planes, capacity=None, stream=None):
-        """Fused forward + zigzag/RLE of up to 4 planes (coefficients never stored).
-        Returns (offsets int32 [N+1], symbols int32 [total]) holding the uint32 bit patterns,
-        blocks numbered plane by plane; capacity defaults to the worst case (64 per block).
-        Reads the total back (one sync)."""
+    def encode_planes(self, planes, outs=None, capacity=None, stream=None):
+        """Forward + zigzag/RLE of up to 4 planes (the count fused into the forward launch).
+        Returns (coefs [int16 [nblk_k, 64]], offsets int32 [N+1], symbols int32 [total]) -- the
+        offsets/symbols hold the uint32 bit patterns, blocks numbered plane by plane; capacity
+        defaults to the worst case (64 per block).  Reads the total back (one sync)."""
         import torch
         n = len(planes)
         descs = (_Plane * n)(*[plane_desc(px) for px in planes])
-        nb = sum(d.nframes * (d.width // 8) * (d.height // 8) for d in descs)
+        nbs = [d.nframes * (d.width // 8) * (d.height // 8) for d in descs]
+        nb = sum(nbs)
         dev = planes[0].device
+        if outs is None:
+            outs = [torch.empty((m, 64), dtype=torch.int16, device=dev) for m in nbs]
         cap = 64 * nb if capacity is None else int(capacity)
         off = torch.empty(nb + 1, dtype=torch.int32, device=dev)
         sym = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
         ws = torch.empty(int(lib().dctq_encode_workspace_bytes(nb)) // 4 + 1, dtype=torch.int32, device=dev)
-        _check(lib().dctq_encode_planes(self._h, descs, n, C.c_void_p(off.data_ptr()), C.c_void_p(sym.data_ptr()),
-                                        cap, C.c_void_p(ws.data_ptr()), _stream_ptr(stream)))
+        cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+        _check(lib().dctq_encode_planes(self._h, descs, n, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
+                                        C.c_void_p(sym.data_ptr()), cap, C.c_void_p(ws.data_ptr()),
+                                        _stream_ptr(stream)))
         total = int(off[nb].item()) & 0xFFFFFFFF
-        return off, sym[:min(total, cap)]
+        return outs, off, sym[:min(total, cap)]
 
     def forward_float(self, px, out=None, stream=None):
         import torch

@@ -297,26 +297,21 @@ size_t dctq_encode_workspace_bytes(long long total_blocks) {
     return dctq::encode_workspace_bytes((total_blocks < 1 ? 1 : total_blocks) / 64 + dctq::kMaxPlanes + 1);
 }
 
-int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *offsets,
-                       uint32_t *symbols, long long symbols_capacity, void *workspace, void *stream) {
+int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                       uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
+                       void *stream) {
     DCTQ_ENTRY;
-    if (!plan || !planes || !offsets || !workspace) return fail(DCTQ_EINVAL, "plan/planes/offsets/workspace is NULL");
-    if (nplanes < 1 || nplanes > dctq::kMaxPlanes) return fail(DCTQ_EINVAL, "nplanes must be in [1, 4]");
+    if (!plan || !offsets || !workspace) return fail(DCTQ_EINVAL, "plan/offsets/workspace is NULL");
     if (symbols_capacity < 0) return fail(DCTQ_EINVAL, "symbols_capacity < 0");
     dctq::EncodeSet es = {};
-    es.ps.n = nplanes;
-    uint32_t first = 0;
+    int rc = plane_set(planes, nplanes, coef, nullptr, &es.ps);
+    if (rc) return rc;
     long long blocks = 0;
     for (int k = 0; k < nplanes; ++k) {
-        int rc = plane_args(&planes[k], &es.ps.pl[k]);
-        if (rc) return rc;
-        es.ps.first[k] = first;
         es.blk_first[k] = (uint32_t)blocks;
-        first += (uint32_t)((es.ps.pl[k].nblk + 63) / 64);
         blocks += es.ps.pl[k].nblk;
         if (blocks >= (1ll << 26)) return fail(DCTQ_EINVAL, "more than 2^26 - 1 blocks in one encode");
     }
-    for (int k = nplanes; k <= dctq::kMaxPlanes; ++k) es.ps.first[k] = first;
     es.blk_first[nplanes] = (uint32_t)blocks;
     HIPCHK(dctq::launch_encode(es, plan->dev, plan->adaptive, offsets, symbols,
                                symbols ? (unsigned long long)symbols_capacity : 0ull, workspace, (hipStream_t)stream,
@@ -404,7 +399,7 @@ int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offset
     DCTQ_ENTRY;
     if (int rc = rle_args(coef, offsets, nblocks)) return rc;
     if (!symbols) return fail(DCTQ_EINVAL, "symbols is NULL");
-    HIPCHK(dctq::launch_rle_emit(coef, nblocks, offsets, symbols, (hipStream_t)stream, device_cus()),
+    HIPCHK(dctq::launch_rle_emit(coef, nblocks, offsets, symbols, ~0ull, (hipStream_t)stream, device_cus()),
            "rle_emit launch");
     return DCTQ_OK;
 }

@@ -320,20 +320,79 @@ __device__ __forceinline__ int pop_flag(uint32_t &mlo, uint32_t &mhi) {
     return (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
 }
 
-// The forward of one 64-block batch with every flagged coefficient resolved IN
-// PLACE (for consumers that read the final ints from the stage in the same
-// launch: the fused round trip and the encoder): fdct8_compute into the stage,
-// the constant-block DC table, then each owning lane recomputes its flagged
-// coefficients in the reference's exact order from the pixels still in its
-// registers.  Returns the number of exact recomputations of this lane.
+// In-place tie resolution, for consumers that read the final ints from the
+// stage in the same launch (the fused round trip and the encoder).  The exact
+// path's tables live in LDS (one 1 KiB copy per workgroup): per-lane global
+// table loads at L2 latency made the first version of that path cost ~40 % of
+// the encoder's count pass.  So the resolution runs AFTER the prefetch fence
+// (its LDS reads must not land in the previous batch's pending store data).
+struct ExactTables {
+    double dct[64];
+    double quant[64];
+};
+
+__device__ __forceinline__ void load_exact_tables(ExactTables *t, const DevTables *__restrict__ dev) {
+    for (int i = threadIdx.x; i < 128; i += blockDim.x)
+        reinterpret_cast<double *>(t)[i] = i < 64 ? dev->dct[i] : dev->quant[i - 64];
+    __syncthreads();
+}
+
+// exact_from_rows() with the tables from LDS.
+template <bool ADAPTIVE>
+__device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c, const ExactTables *tab) {
+    const int i = c >> 3, j = c & 7;
+    double dj[8], di[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        dj[k] = tab->dct[j * 8 + k];  // D^T[k][j]
+        di[k] = tab->dct[i * 8 + k];  // D[i][k]
+    }
+    double m = tab->quant[c];
+    if (ADAPTIVE && c != 0) {
+        uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s1 = __builtin_amdgcn_udot4(rows[k].x, 0x01010101u, s1, false);
+            s1 = __builtin_amdgcn_udot4(rows[k].y, 0x01010101u, s1, false);
+            s2 = __builtin_amdgcn_udot4(rows[k].x, rows[k].x, s2, false);
+            s2 = __builtin_amdgcn_udot4(rows[k].y, rows[k].y, s2, false);
+        }
+        const int32_t sx = (int32_t)s1 - 8192;
+        const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
+        m = m * adaptive_scale(64 * sxx - sx * sx);
+        if (m < 1.0) m = 1.0;
+    }
+    double out = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        double t = 0.0;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const uint32_t w = l < 4 ? rows[k].x : rows[k].y;
+            t += ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
+        }
+        out += di[k] * t;
+    }
+    return (int)round(out / m);
+}
+
+// Phase 1: the forward of one 64-block batch into the stage plus the constant-
+// block DC table; returns the lane's remaining tie flags (none for invalid lanes).
 template <bool ADAPTIVE, bool VAR>
-__device__ __forceinline__ uint32_t forward_exact_batch(const DevTables *__restrict__ dev, const uint2 (&cur)[8],
-                                                        uint4 *stage, int lane, int wv, bool valid,
-                                                        int32_t &var_num) {
-    uint32_t mlo, mhi;
+__device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict__ dev, const uint2 (&cur)[8],
+                                                    uint4 *stage, int lane, int wv, bool valid, int32_t &var_num,
+                                                    uint32_t &mlo, uint32_t &mhi) {
     fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
     flat_dc_fix(dev, cur, stage, lane, wv, mlo);
     if (!valid) mlo = mhi = 0;
+}
+
+// Phase 2 (after the prefetch fence): each owning lane recomputes its flagged
+// coefficients in the reference's exact order from the pixels still in its
+// registers and patches the stage.  Returns the lane's recomputation count.
+template <bool ADAPTIVE>
+__device__ __forceinline__ uint32_t resolve_ties(const ExactTables *tab, const uint2 (&cur)[8], uint4 *stage,
+                                                 int lane, int wv, uint32_t mlo, uint32_t mhi) {
     uint32_t n = 0;
     if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) {
         int16_t *mine16 = reinterpret_cast<int16_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 2);
@@ -347,7 +406,7 @@ __device__ __forceinline__ uint32_t forward_exact_batch(const DevTables *__restr
                 rows[r] = cur[r];
                 asm volatile("" : "+v"(rows[r].x), "+v"(rows[r].y));
             }
-            mine16[c] = (int16_t)exact_from_rows<ADAPTIVE>(rows, c, dev);
+            mine16[c] = (int16_t)exact_from_rows_lds<ADAPTIVE>(rows, c, tab);
             ++n;
         }
     }

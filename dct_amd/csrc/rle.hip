@@ -203,7 +203,8 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                const uint32_t *__restrict__ offsets,
-                                                               uint32_t *__restrict__ symbols, long long ntiles) {
+                                                               uint32_t *__restrict__ symbols, long long ntiles,
+                                                               unsigned long long capacity) {
     __shared__ u4r tiles_lds[kRleWaves][64 * 8];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long stride = (long long)gridDim.x * kRleWaves;
@@ -239,10 +240,12 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
                    ((uint32_t)*reinterpret_cast<const uint16_t *>(lt + (2 * u + 1) * 128 + zoff) << 16);
         const int nb = tile_blocks(t, nblk);
         // the tile's symbols start at offsets[64t]: a per-tile descriptor keeps the
-        // 32-bit voffset small (the stream itself may exceed 4 GiB)
+        // 32-bit voffset small (the stream itself may exceed 4 GiB); symbols at or
+        // past `capacity` are dropped by num_records
         const uint32_t o0 = __builtin_amdgcn_readlane(offv, 0);
-        const __amdgpu_buffer_rsrc_t rsym =
-            __builtin_amdgcn_make_buffer_rsrc(symbols + o0, (short)0, 64 * 64 * 4, 0x00020000);
+        const unsigned long long room = capacity > o0 ? capacity - o0 : 0ull;
+        const __amdgpu_buffer_rsrc_t rsym = __builtin_amdgcn_make_buffer_rsrc(
+            symbols + o0, (short)0, (int)((room < 4096ull ? room : 4096ull) * 4u), 0x00020000);
 #pragma unroll
         for (int u = 0; u < 64; ++u) {
             const uint32_t val = (u & 1) ? z[u >> 1] >> 16 : z[u >> 1] & 0xFFFFu;
@@ -374,10 +377,10 @@ hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offse
 }
 
 hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,
-                           hipStream_t stream, int num_cus) {
+                           unsigned long long capacity, hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
     hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, coef, nblk,
-                       offsets, symbols, ntiles);
+                       offsets, symbols, ntiles, capacity);
     return hipGetLastError();
 }
 

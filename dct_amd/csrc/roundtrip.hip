@@ -94,6 +94,8 @@ template <bool ADAPTIVE, bool VAR, bool STATS>
 __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet rt, const DevTables *__restrict__ dev,
                                                           unsigned long long *fallbacks) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ ExactTables tab;
+    load_exact_tables(&tab, dev);
     const PlaneSet &ps = rt.ps;
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5, j = lane & 31;
@@ -118,9 +120,11 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
 
         // ---- 1. forward into the stage; ties resolved in place
         int32_t var_num;
-        const uint32_t ne = forward_exact_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num);
+        uint32_t mlo, mhi;
+        forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
+        retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
+        const uint32_t ne = resolve_ties<ADAPTIVE>(&tab, cur, stage, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
-        retire_stores();  // the previous batch's recon stores (long issued) before the read-back
         wave_sync();
 
         // ---- 2. read-back: coefficient chunks + the inverse's half blocks

@@ -86,21 +86,22 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
 int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                            int32_t *const *var_num, float *const *recon, void *stream);
 
-/* Fused encoder: forward DCT + quantization + zigzag run-length
- * symbols of up to 4 planes, the coefficients never written to HBM.  Blocks are
- * numbered plane 0 first, then plane 1, ... (N in total, N < 2^26):
+/* Encoder: forward DCT + quantization + zigzag run-length
+ * symbols of up to 4 planes.  coef[k] exactly as dctq_forward_quant_planes;
+ * blocks numbered plane 0 first, then plane 1, ... (N in total, N < 2^26):
  *   offsets[b]  = first symbol of block b, offsets[N] = total symbols
  *   symbols[..] = the reference's run_length_encode of every block, in order,
- *                 (uint16)value | run << 16 (as dctq_rle_emit over the planes'
- *                 dctq_forward_quant output)
- * Symbols at index >= symbols_capacity are not written; offsets are always
- * complete (compare offsets[N] with the capacity).  symbols == NULL or capacity
- * 0: offsets only.  Worst case 64 symbols per block.  workspace:
- * dctq_encode_workspace_bytes(N) bytes.  Two passes over the pixels (the
- * forward recomputed instead of stored). */
+ *                 (uint16)value | run << 16 (as dctq_rle_count + dctq_rle_emit
+ *                 over the concatenated coefficient planes)
+ * The symbol count is fused into the forward launch.  Symbols at index >=
+ * symbols_capacity are not written; offsets are always complete (compare
+ * offsets[N] with the capacity).  symbols == NULL or capacity 0: coefficients
+ * and offsets only.  Worst case 64 symbols per block.  workspace:
+ * dctq_encode_workspace_bytes(N) bytes. */
 size_t dctq_encode_workspace_bytes(long long total_blocks);
-int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *offsets,
-                       uint32_t *symbols, long long symbols_capacity, void *workspace, void *stream);
+int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                       uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
+                       void *stream);
 
 /* Forward DCT only, float coefficients coef[f][by][bx][64]
  * (|coef - dct_forward()| <= 1e-4; computed in fp64, rounded once to fp32). */

@@ -579,7 +579,7 @@ def test_rle_large_planes(T, dm):
 
 
 def test_encode_planes_fused(T, dm):
-    """dctq_encode_planes (forward + zigzag/RLE, coefficients never stored) equals the
+    """dctq_encode_planes (forward + zigzag/RLE, the count fused into the forward) equals the
     oracle's run_length_encode of the oracle's quantized planes, blocks numbered plane
     by plane: ragged planes, a frame stack, tie-heavy step blocks (ties resolved before
     counting: a tie can decide zero vs nonzero), adaptive plans."""
@@ -594,7 +594,8 @@ def test_encode_planes_fused(T, dm):
             want = np.concatenate([np.concatenate([O.forward_plane(f, q, ad) for f in (p if p.ndim == 3 else [p])])
                                    for p in planes])
             woff, wsym = O.rle_encode_plane(want)
-            off, sym = plan.encode_planes([gpu_px(T, p) for p in planes])
+            coefs, off, sym = plan.encode_planes([gpu_px(T, p) for p in planes])
+            assert np.array_equal(T.cat(coefs).cpu().numpy(), want), (q, ad)
             assert np.array_equal(off.cpu().numpy().view(np.uint32), woff), (q, ad)
             assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), (q, ad)
 
@@ -606,15 +607,16 @@ def test_encode_capacity_and_large(T, dm):
     import oracle as O
     px = gpu_px(T, O.synth_plane(12, 0, 256, 128))
     plan = dm.Plan(50, 0)
-    off, sym = plan.encode_planes([px])
+    _, off, sym = plan.encode_planes([px])
     total = int(off[-1].item())
-    off2, sym2 = plan.encode_planes([px], capacity=total // 3)
+    _, off2, sym2 = plan.encode_planes([px], capacity=total // 3)
     assert np.array_equal(off.cpu().numpy(), off2.cpu().numpy())
     assert sym2.numel() == total // 3 and np.array_equal(sym2.cpu().numpy(), sym[:total // 3].cpu().numpy())
     luma = dm.synth(13, "uniform", 3840, 2160, 5)
     chroma = dm.synth(14, "smooth", 1920, 1080, 3)
-    off, sym = plan.encode_planes([luma, chroma])
+    ecoefs, off, sym = plan.encode_planes([luma, chroma])
     coefs = plan.forward_quant_planes([luma, chroma])
+    assert all(T.equal(a, b) for a, b in zip(ecoefs, coefs))
     woff, wsym = dm.rle_encode(T.cat(coefs).contiguous())
     assert T.equal(off, woff)
     assert T.equal(sym, wsym)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Fused encoder (dctq_encode_planes) vs the unfused pipeline (forward_quant +
+"""Encoder with the count fused into the forward (dctq_encode_planes) vs the unfused pipeline (forward_quant +
 rle_count + rle_emit) on 64 4K luma planes, uniform and smooth, HIP events;
 bytes per block are each path's algorithmic HBM traffic."""
 import ctypes as C
@@ -37,12 +37,13 @@ for kind in ("uniform", "smooth"):
                                C.c_void_p(sym_buf.data_ptr()), s) == 0
 
     def fused():
-        assert L.dctq_encode_planes(plan._h, d, 1, C.c_void_p(off2.data_ptr()), C.c_void_p(sym_buf.data_ptr()),
-                                    total + 64, C.c_void_p(wse.data_ptr()), s) == 0
+        cp = (C.c_void_p * 1)(coef.data_ptr())
+        assert L.dctq_encode_planes(plan._h, d, 1, C.cast(cp, C.c_void_p), C.c_void_p(off2.data_ptr()),
+                                    C.c_void_p(sym_buf.data_ptr()), total + 64, C.c_void_p(wse.data_ptr()), s) == 0
 
     spb = 4.0 * total / nblk
     jobs = {"unfused forward+count+emit": (unfused, 192 + 140 + 132 + spb),
-            "fused encode (2 passes)": (fused, 64 + 4 + 8 + 64 + 4 + spb)}
+            "encode (count fused)": (fused, 192 + 4 + 8 + 132 + spb)}
     for name, (fn, bpb) in jobs.items():
         fn()
         torch.cuda.synchronize()
