@@ -14,7 +14,9 @@ each rank its own F frames (weak scaling, no data-path collective); value =
 all blocks / max-over-ranks wall time.  A separately reported leg
 ("round_trip", BASELINE configs[4]) runs forward DCT+quant then dequant+IDCT
 over the same frames in ONE fused launch (dctq_round_trip_planes) and reports
-end-to-end blocks/s (the unfused two-kernel pair timed beside it) and PSNR.  At N>1 a
+end-to-end blocks/s (the unfused two-kernel pair timed beside it) and PSNR.
+Another ("encode") runs the encoder (forward + zigzag run-length
+symbols) over the frames, and at N>1 the all-gather of the symbol streams.  At N>1 a
 second, separately reported leg ("gather") times forward DCT+quant of the luma frames followed by the RCCL
 all-gather of every rank's int16 coefficient planes (BASELINE configs[3],
 SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange.
@@ -58,6 +60,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
+    ap.add_argument("--encode-steps", type=int, default=3,
+                    help="timed steps of the encoder leg (forward + zigzag/RLE symbols; at N>1 plus the "
+                         "symbol-stream all-gather); 0 = skip")
     ap.add_argument("--round-trip-steps", type=int, default=3,
                     help="timed steps of the config-5 round trip leg (forward+inverse, PSNR); 0 = skip")
     ap.add_argument("--per-plane", action="store_true",
@@ -126,6 +131,69 @@ def gather_leg(args, plan, luma, coef_y, world, rank, dev):
             "blocks_per_s": world * n * args.gather_steps / el, "ms_per_step": el / args.gather_steps * 1e3,
             "bytes_received_per_rank": (world - 1) * n * 128, "steps": args.gather_steps,
             "own_slice_intact": ok}
+
+
+def encode_leg(args, plan, luma, chroma, world, dev):
+    """the encoder over the frame stream -- dctq_encode_planes
+    (forward + zigzag run-length symbols of reference semantics, the symbol count
+    fused into the forward launch) -- and at N>1 the all-gather of every rank's
+    symbol stream (shard.gather_symbols), end to end, max over ranks.  Reports the
+    stream size against the int16 coefficient planes (the bench's uniform input
+    is the RLE worst case: most coefficients are nonzero)."""
+    import ctypes as C
+    from dct_amd import shard
+    L = dct_amd.lib()
+    pls = [luma, chroma]
+    descs = (dct_amd._Plane * 2)(*[dct_amd.plane_desc(p) for p in pls])
+    nbs = [p.shape[0] * (p.shape[1] // 8) * (p.shape[2] // 8) for p in pls]
+    n = sum(nbs)
+    coefs = [torch.empty((m, 64), dtype=torch.int16, device=dev) for m in nbs]
+    off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    cap = 64 * n
+    sym = torch.empty(cap, dtype=torch.int32, device=dev)
+    ws = torch.empty(int(L.dctq_encode_workspace_bytes(n)) // 4 + 1, dtype=torch.int32, device=dev)
+    cp = (C.c_void_p * 2)(*[c.data_ptr() for c in coefs])
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def encode():
+        rc = L.dctq_encode_planes(plan._h, descs, 2, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
+                                  C.c_void_p(sym.data_ptr()), cap, C.c_void_p(ws.data_ptr()), stream)
+        if rc:
+            raise RuntimeError(f"dctq_encode_planes rc={rc}")
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.encode_steps):
+            fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    el = timed(encode)
+    total = int(off[n].item()) & 0xFFFFFFFF
+    out = {"op": "encode_planes (forward + zigzag/RLE, count fused) over all planes", "steps": args.encode_steps,
+           "blocks_per_s": world * n * args.encode_steps / el, "ms_per_step": el / args.encode_steps * 1e3,
+           "symbols_per_block": total / n, "stream_bytes_per_block": 4.0 * (1 + total / n),
+           "coefficient_bytes_per_block": 128}
+    if world > 1:
+        def encode_gather():
+            encode()
+            return shard.gather_symbols(off, sym)
+        el2 = timed(encode_gather)
+        out.update({"gather_op": "encode + symbol-stream all_gather ("
+                                 + ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()) + ")",
+                    "gather_blocks_per_s": world * n * args.encode_steps / el2,
+                    "gather_ms_per_step": el2 / args.encode_steps * 1e3})
+    return out
 
 
 def round_trip_leg(args, plan, luma, chroma, world, dev):
@@ -275,6 +343,10 @@ def main():
     if world > 1 and args.gather_steps > 0:
         gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
 
+    encode = None
+    if args.encode_steps > 0:
+        encode = encode_leg(args, plan, luma, chroma, world, dev)
+
     round_trip = None
     if args.round_trip_steps > 0:
         round_trip = round_trip_leg(args, plan, luma, chroma, world, dev)
@@ -318,6 +390,7 @@ def main():
             "parity_check": parity,
             "gather": gather,
             "round_trip": round_trip,
+            "encode": encode,
             "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
                     "reference-order recomputation for guard-band (tie) coefficients",
         }

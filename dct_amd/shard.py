@@ -8,11 +8,13 @@ src/quantization.c:113-131), so the path partitions with no data exchange:
   itself a plane (pixel pointer advanced by 8*row0*stride, height 8*rows), and
   its coefficients are a contiguous slice of the raster-order output.
 
-The only collective is the OPTIONAL gather of the int16 coefficient planes
+The only collectives are OPTIONAL gathers: of the int16 coefficient planes
 (BASELINE configs[3]: "RCCL allgather of quantized coefficient planes over
-xGMI"): one all_gather per call over the whole shard, padded to the largest
-shard so ragged splits work.  The ordering of the gathered result equals the
-unsharded raster order, so rank r's slice lands at blocks_before(r).
+xGMI"), or of the run-length symbol streams the encoder makes of them (SURVEY
+8(f)3: shrink the bytes before the exchange).  Each is one all_gather per call
+over the whole shard, padded to the largest shard so ragged splits work.  The
+ordering of the gathered result equals the unsharded raster order, so rank r's
+slice lands at blocks_before(r).
 """
 from __future__ import annotations
 
@@ -75,3 +77,53 @@ def gather_coefficients(local, counts, group=None):
     if all(c == m for c in counts):
         return torch.cat(parts)
     return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+
+def _all_gather_padded(send, m, group):
+    """all_gather of equally sized (padded) 1-D/2-D shards; raw bytes over gloo."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world * m,) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+        dist.all_gather_into_tensor(out, send, group=group)
+        return list(out.split(m))
+    raw = send.view(torch.uint8)
+    parts = [torch.empty_like(raw) for _ in range(world)]
+    dist.all_gather(parts, raw, group=group)
+    return [p.view(send.dtype) for p in parts]
+
+
+def gather_symbols(offsets, symbols, group=None):
+    """All-gather every rank's run-length stream (dctq_encode_planes / rle_encode:
+    offsets [n_r + 1], symbols [offsets[n_r]], int32 holding uint32 bit patterns)
+    into the stream of the unsharded input on every rank: (offsets [N + 1],
+    symbols [total]), rank r's offsets shifted by the symbols of ranks < r.
+
+    Two collectives: the per-rank sizes (2 int64), then the padded streams --
+    offsets and symbols travel in one buffer, so a shard costs 4 B per block
+    plus 4 B per symbol on the wire instead of 128 B per block."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = offsets.numel() - 1
+    total = int(offsets[n].item()) & 0xFFFFFFFF
+    if symbols.numel() < total:
+        raise ValueError("symbols shorter than offsets[n]")
+    dev = offsets.device
+    sizes = torch.tensor([n, total], dtype=torch.int64, device=dev)
+    allsz = _all_gather_padded(sizes.view(1, 2), 1, group)
+    ns = [int(t[0, 0]) for t in allsz]
+    tots = [int(t[0, 1]) for t in allsz]
+    m = max(a + b for a, b in zip(ns, tots))
+    send = torch.zeros(m, dtype=torch.int32, device=dev)
+    send[:n] = offsets[:n]
+    send[n:n + total] = symbols[:total]
+    parts = _all_gather_padded(send, m, group)
+    offs, syms, base = [], [], 0
+    for p, nr, tr in zip(parts, ns, tots):
+        offs.append((p[:nr].to(torch.int64) & 0xFFFFFFFF) + base)
+        syms.append(p[nr:nr + tr])
+        base += tr
+    offs.append(torch.tensor([base], dtype=torch.int64, device=dev))
+    return torch.cat(offs).to(torch.int32), torch.cat(syms)

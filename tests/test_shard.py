@@ -49,6 +49,16 @@ def _worker(rank, world, port, q):
         counts = [shard.split(7, world, r)[1] * 8 - shard.split(7, world, r)[0] * 8 for r in range(world)]
         full = shard.gather_coefficients(local, counts)
         assert np.array_equal(full.numpy(), O.forward_plane(plane.numpy(), 90, 1)), "band-sharded gather differs"
+
+        # (3) run-length streams of the frame shards (what dctq_encode_planes makes on each GPU)
+        mine, (lo, hi) = shard.frame_shard(frames, world, rank)
+        local = (np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in mine])
+                 if hi > lo else np.zeros((0, 64), np.int16))
+        loff, lsym = O.rle_encode_plane(local)
+        off, sym = shard.gather_symbols(torch.from_numpy(loff.view(np.int32)), torch.from_numpy(lsym.view(np.int32)))
+        woff, wsym = O.rle_encode_plane(np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in frames]))
+        assert np.array_equal(off.numpy().view(np.uint32), woff), "gathered offsets differ"
+        assert np.array_equal(sym.numpy().view(np.uint32), wsym), "gathered symbols differ"
         q.put((rank, "ok"))
     except BaseException as e:  # noqa: BLE001 -- report to the parent
         q.put((rank, repr(e)))
