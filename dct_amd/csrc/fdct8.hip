@@ -197,7 +197,13 @@ __global__ __launch_bounds__(kThreads) void fdct8_quant_v1(PlaneArgs p, FastTabl
 //  * the LDS stage is written out as 1 KiB-contiguous buffer stores (num_records
 //    clips the tail, so the stores are unconditional);
 //  * flagged (block, coefficient) pairs go to a wave-local LDS queue and are
-//    recomputed exactly 64 at a time (every lane busy), then patched in HBM.
+//    recomputed exactly 64 at a time (every lane busy), then patched in HBM;
+//  * one launch covers up to 4 planes (PlaneSet): the grid-stride index runs
+//    over the concatenated 64-block batches, each batch finding its plane by
+//    wave-uniform compares against the planes' batch prefixes.
+// The per-batch building blocks (block addressing, row loads, the arithmetic
+// into the stage, the constant-block DC fix) are in fdct8_core.h.
+
 // Exact reference-order quantization of coefficient c of the block at px (one
 // queue entry): exact_from_rows() over the pixels stashed when it was queued.
 // A drain runs 64 of these at once (one per lane), so latency matters: all 8
