@@ -133,6 +133,41 @@ def gather_leg(args, plan, luma, coef_y, world, rank, dev):
             "own_slice_intact": ok}
 
 
+def small_frame_leg(args, plan, dev):
+    """BASELINE configs[1]: one 512x512 grayscale frame (4 096 blocks, 256 KiB in,
+    512 KiB out: cache-resident, so launch-bound -- not an HBM-roofline figure),
+    200 back-to-back dctq_forward_quant launches, next to the reference's CPU
+    path on the same frame (oracle/_ref, 16 threads, rank 0 only)."""
+    import numpy as np
+    import oracle as O
+    px = dct_amd.synth(args.seed + 7, args.kind, 512, 512, device=dev)
+    out = torch.empty((4096, 64), dtype=torch.int16, device=dev)
+    n = 200
+    for _ in range(10):
+        plan.forward_quant(px, out=out)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        plan.forward_quant(px, out=out)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = {"frame": "512x512 u8 (4096 blocks)", "launches": n, "us_per_frame": el / n * 1e6,
+           "blocks_per_s": 4096 * n / el}
+    host = px[0].cpu().numpy()
+    got = out.cpu().numpy()
+    if O.ref_available():
+        ref = np.zeros((4096, 64), np.int16)
+        threads = max(1, min(16, os.cpu_count() or 1))
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 1.0:
+            O.ref().ref_forward_plane(np.ascontiguousarray(host).ravel(), 512, 512, args.quality, args.adaptive,
+                                      ref.ravel(), threads, 0)
+            reps += 1
+        res.update({"cpu_reference_blocks_per_s": 4096 * reps / (time.perf_counter() - t0), "cpu_threads": threads,
+                    "bit_exact_vs_reference": bool(np.array_equal(got, ref))})
+    return res
+
+
 def encode_leg(args, plan, luma, chroma, world, dev):
     """the encoder over the frame stream -- dctq_encode_planes
     (forward + zigzag run-length symbols of reference semantics, the symbol count
@@ -343,6 +378,8 @@ def main():
     if world > 1 and args.gather_steps > 0:
         gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
 
+    small = small_frame_leg(args, plan, dev) if rank == 0 and not args.no_cpu else None
+
     encode = None
     if args.encode_steps > 0:
         encode = encode_leg(args, plan, luma, chroma, world, dev)
@@ -391,6 +428,7 @@ def main():
             "gather": gather,
             "round_trip": round_trip,
             "encode": encode,
+            "small_frame": small,
             "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
                     "reference-order recomputation for guard-band (tie) coefficients",
         }
