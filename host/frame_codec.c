@@ -3,7 +3,10 @@
  * (include/dct_amd.h): generates a synthetic frame on the device, runs the
  * forward DCT+quant hot path and the inverse, and prints a 64-bit FNV-1a
  * checksum of the int16 coefficient plane plus the round-trip PSNR
- * (tests/test_entropy.c:376-393 formula, clamped recon).
+ * (tests/test_entropy.c:376-393 formula, clamped recon).  Then the same frame
+ * through the fused round trip (dctq_round_trip_planes: must reproduce the
+ * coefficients and the recon of the two calls) and the encoder
+ * (dctq_encode_planes: run-length symbol count and an FNV-1a of the stream).
  *
  *   frame_codec WIDTH HEIGHT QUALITY ADAPTIVE SEED [KIND]
  */
@@ -65,6 +68,54 @@ int main(int argc, char **argv) {
     double mse = se / ((double)w * h);
     printf("fnv1a:%016llx\n", (unsigned long long)fnv);
     printf("psnr:%.4f\n", 10.0 * __builtin_log10(255.0 * 255.0 / mse));
+
+    /* fused round trip: one launch, same coefficients, same recon within 1e-4 */
+    void *coef2, *rec2;
+    CHK(dctq_malloc(&coef2, (size_t)nblk * 128));
+    CHK(dctq_malloc(&rec2, (size_t)nblk * 256));
+    int16_t *c2p = (int16_t *)coef2;
+    float *r2p = (float *)rec2;
+    CHK(dctq_round_trip_planes(plan, &pl, 1, &c2p, NULL, &r2p, NULL));
+    CHK(dctq_synchronize(NULL));
+    int16_t *hc2 = malloc((size_t)nblk * 128);
+    float *hr2 = malloc((size_t)nblk * 256);
+    CHK(dctq_memcpy_dtoh(hc2, coef2, (size_t)nblk * 128));
+    CHK(dctq_memcpy_dtoh(hr2, rec2, (size_t)nblk * 256));
+    int same = 1;
+    double maxd = 0.0;
+    for (long long i = 0; i < nblk * 64; ++i) {
+        same &= hc2[i] == hc[i];
+        double d = hr2[i] - hr[i];
+        if (d < 0) d = -d;
+        if (d > maxd) maxd = d;
+    }
+    printf("fused:%s\n", same && maxd <= 1e-4 ? "ok" : "MISMATCH");
+
+    /* encoder: coefficients + zigzag run-length symbols */
+    void *off, *sym, *ws;
+    const long long cap = 64 * nblk;
+    CHK(dctq_malloc(&off, (size_t)(nblk + 1) * 4));
+    CHK(dctq_malloc(&sym, (size_t)cap * 4));
+    CHK(dctq_malloc(&ws, dctq_encode_workspace_bytes(nblk)));
+    CHK(dctq_encode_planes(plan, &pl, 1, &c2p, (uint32_t *)off, (uint32_t *)sym, cap, ws, NULL));
+    CHK(dctq_synchronize(NULL));
+    uint32_t total = 0;
+    CHK(dctq_memcpy_dtoh(&total, (const char *)off + (size_t)nblk * 4, 4));
+    uint32_t *hs = malloc((size_t)total * 4 + 4);
+    CHK(dctq_memcpy_dtoh(hs, sym, (size_t)total * 4));
+    uint64_t fs = 1469598103934665603ULL;
+    const uint8_t *sb = (const uint8_t *)hs;
+    for (long long i = 0; i < (long long)total * 4; ++i) fs = (fs ^ sb[i]) * 1099511628211ULL;
+    printf("symbols:%u\n", total);
+    printf("symbols_fnv1a:%016llx\n", (unsigned long long)fs);
+    dctq_free(coef2);
+    dctq_free(rec2);
+    dctq_free(off);
+    dctq_free(sym);
+    dctq_free(ws);
+    free(hc2);
+    free(hr2);
+    free(hs);
     dctq_plan_destroy(plan);
     dctq_free(px);
     dctq_free(coef);

@@ -362,6 +362,22 @@ def test_invalid_arguments(T, dm):
         plan.forward_quant(torch.zeros((16, 16), dtype=torch.uint8, device="cuda")[:, 1:9])
     with pytest.raises(dm.DctqError):
         dm.Plan(50, 1).inverse(torch.zeros((4, 64), dtype=torch.int16, device="cuda"))
+    # the multi-plane calls: 0 or 5 planes, a bad plane among good ones, NULL outputs
+    g = torch.zeros((16, 16), dtype=torch.uint8, device="cuda")
+    for fn in (plan.round_trip_planes, plan.encode_planes):
+        with pytest.raises(dm.DctqError):
+            fn([g] * 5)
+        with pytest.raises(dm.DctqError):
+            fn([g, torch.zeros((12, 16), dtype=torch.uint8, device="cuda")])
+    L = dm.lib()
+    d = (dm._Plane * 1)(dm.plane_desc(g))
+    o = torch.empty((4, 64), dtype=torch.int16, device="cuda")
+    cp = C.cast((C.c_void_p * 1)(o.data_ptr()), C.c_void_p)
+    assert L.dctq_round_trip_planes(plan._h, d, 1, cp, None, None, None) != 0           # recon array NULL
+    off = torch.empty(5, dtype=torch.int32, device="cuda")
+    assert L.dctq_encode_planes(plan._h, d, 1, cp, C.c_void_p(off.data_ptr()), None, 0, None, None) != 0  # no ws
+    assert L.dctq_encode_planes(plan._h, d, 1, cp, C.c_void_p(off.data_ptr()), None, -1, C.c_void_p(off.data_ptr()),
+                                None) != 0                                                 # negative capacity
 
 
 # ------------------------------------------------------------ legacy per-block API
@@ -511,6 +527,12 @@ def test_c_host_programs(T, dm, blocks, tmp_path):
         for b in want:
             fnv = ((fnv ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
         assert int(got["fnv1a"], 16) == fnv, (w, h, q, ad)
+        assert got["fused"] == "ok", (w, h, q, ad)
+        _, wsym = O.rle_encode_plane(np.frombuffer(want, np.int16).reshape(-1, 64))
+        fs = 1469598103934665603
+        for b in wsym.tobytes():
+            fs = ((fs ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+        assert int(got["symbols"]) == wsym.size and int(got["symbols_fnv1a"], 16) == fs, (w, h, q, ad)
 
 
 @pytest.mark.parametrize("prog", ["dct", "quantization", "entropy"])
