@@ -60,7 +60,9 @@ FastDiv make_fastdiv(uint32_t d) {
 // satisfies |V - (r + f~)| <= B below; hence |f~| <= 0.5 - B  =>  round(V) == r.
 void fill_fast_tables(const double *q, int adaptive, FastTables *t) {
     const double u = 0x1p-24;
-    const double rel = adaptive ? 3.0 * u + 0x1p-48 : u + 0x1p-48;
+    // scale-factor representation: fl32(w) (0.5u) and its product (0.5u); adaptive
+    // plans also the kernel's 1/(2-nv) = v_rcp_f32(fl32(2-nv)) (0.5u + 2u, fdct8_core.h)
+    const double rel = adaptive ? 4.5 * u + 0x1p-48 : u + 0x1p-48;
     for (int c = 0; c < 64; ++c) {
         const int i = c >> 3, j = c & 7;
         const double w = kAanScale[i] * kAanScale[j] / q[c];

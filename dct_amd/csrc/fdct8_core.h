@@ -190,7 +190,14 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
 
     f2 sc2 = {1.0f, 1.0f};
     if (ADAPTIVE) {
-        const float inv = (float)(1.0 / adaptive_scale(var_num));
+        // The fast path only needs 1/(2-nv) within its guard band (4.5u relative for
+        // adaptive plans, api.hip fill_fast_tables): nv through a multiply by
+        // fl(0.001) instead of the reference's division (relative error ~2^-52),
+        // then fl32(2-nv) (0.5u) and v_rcp_f32 (1 ulp = 2u) -- two fp64 divisions
+        // per lane per batch were ~8 % of the adaptive kernel's time.  The exact
+        // path keeps the reference's arithmetic (adaptive_scale).
+        const double nv = fmin(1.0, fmax(0.1, (double)var_num * (1.0 / 4096.0) * 0.001));
+        const float inv = __builtin_amdgcn_rcpf((float)(2.0 - nv));
         sc2 = f2{inv, inv};
     }
     // Per-plan tables through an opaque per-batch pointer in the constant address
