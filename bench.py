@@ -378,7 +378,7 @@ def main():
     if world > 1 and args.gather_steps > 0:
         gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
 
-    small = small_frame_leg(args, plan, dev) if rank == 0 and not args.no_cpu else None
+    small = small_frame_leg(args, plan, dev) if world == 1 and not args.no_cpu else None  # single-GPU config
 
     encode = None
     if args.encode_steps > 0:
@@ -400,7 +400,7 @@ def main():
         except Exception:
             traffic = None
     if rank == 0:
-        cpu = None if args.no_cpu else cpu_baseline(args)
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args)  # rank 0 at N=1 only
         out = {
             "metric": "8x8 macroblocks/sec (DCT+quant); % HBM roofline",
             "value": value,
