@@ -642,3 +642,44 @@ def test_encode_capacity_and_large(T, dm):
     woff, wsym = dm.rle_encode(T.cat(coefs).contiguous())
     assert T.equal(off, woff)
     assert T.equal(sym, wsym)
+
+
+def test_randomized_sweep_all_planes_apis(T, dm):
+    """40 random configurations (kinds, qualities 1-100, adaptive, 1-4 planes of
+    ragged geometry, frame stacks, padded rows) through forward_quant_planes,
+    round_trip_planes and encode_planes, all against the oracle."""
+    import oracle as O
+    import torch
+    rng = np.random.default_rng(2026)
+    for trial in range(40):
+        q = int(rng.integers(1, 101))
+        ad = int(rng.integers(0, 2))
+        nplanes = int(rng.integers(1, 5))
+        planes, hosts = [], []
+        for _ in range(nplanes):
+            w, h = 8 * int(rng.integers(1, 48)), 8 * int(rng.integers(1, 24))
+            nf = int(rng.integers(1, 4))
+            pad = 8 * int(rng.integers(0, 3))
+            kind = int(rng.integers(0, 4))
+            frames = [O.synth_plane(int(rng.integers(1, 1 << 30)), kind, w, h) for _ in range(nf)]
+            buf = torch.zeros((nf, h, w + pad), dtype=torch.uint8)
+            for f in range(nf):
+                buf[f, :, :w] = torch.from_numpy(frames[f])
+            planes.append(buf.cuda()[:, :, :w])
+            hosts.append(frames)
+        plan = dm.Plan(q, ad)
+        want = [np.concatenate([O.forward_plane(f, q, ad) for f in fr]) for fr in hosts]
+        got = plan.forward_quant_planes(planes)
+        for g, wv in zip(got, want):
+            assert np.array_equal(g.cpu().numpy(), wv), ("forward", trial, q, ad)
+        coefs, recs = plan.round_trip_planes(planes)
+        for c, r, wv, fr in zip(coefs, recs, want, hosts):
+            assert np.array_equal(c.cpu().numpy(), wv), ("round trip", trial, q, ad)
+            var = np.concatenate([O.plane_variance(f) for f in fr]) if ad else None
+            ref = O.inverse_plane(wv, q, ad, var) + 128.0
+            assert np.abs(r.cpu().numpy().astype(np.float64) - ref).max() <= 1e-4, ("recon", trial, q, ad)
+        ecoefs, off, sym = plan.encode_planes(planes)
+        woff, wsym = O.rle_encode_plane(np.concatenate(want))
+        assert all(np.array_equal(c.cpu().numpy(), wv) for c, wv in zip(ecoefs, want)), ("encode coef", trial)
+        assert np.array_equal(off.cpu().numpy().view(np.uint32), woff), ("encode offsets", trial, q, ad)
+        assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), ("encode symbols", trial, q, ad)
