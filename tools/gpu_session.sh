@@ -21,7 +21,7 @@ for step in "$@"; do
   case $step in
     info) run info 60 bash -c "rocm-smi --showproductname --showclocks 2>&1 | head -40; nproc; lscpu | grep 'Model name'" ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    test) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
+    test) run pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     testall) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
     bench) run bench 600 python bench.py ;;
     benchq) run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu ;;
@@ -43,6 +43,8 @@ for step in "$@"; do
     ceil) run ceil 120 tools/ubench/stream_ceiling ;;
     ceil2) run ceil2 120 tools/ubench/stream_ceiling2 ;;
     ceil3) run ceil3 120 tools/ubench/stream_ceiling3 ;;
+    ceil4) run ceil4 180 tools/ubench/stream_ceiling4 ;;
+    planes) run planes 300 python tools/plane_bench.py ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
     enc) run enc 300 python tools/enc_bench.py ;;
