@@ -65,6 +65,8 @@ def parse():
                          "symbol-stream all-gather); 0 = skip")
     ap.add_argument("--round-trip-steps", type=int, default=3,
                     help="timed steps of the config-5 round trip leg (forward+inverse, PSNR); 0 = skip")
+    ap.add_argument("--ceiling-rounds", type=int, default=10,
+                    help="interleaved forward / no-arithmetic movement launches for roofline.movement_ceiling (0 = skip)")
     ap.add_argument("--per-plane", action="store_true",
                     help="two launches per step (luma, then chroma) instead of one multi-plane launch")
     ap.add_argument("--backend", default="nccl", help="N>1 process group (nccl = RCCL; gloo only to rehearse "
@@ -293,6 +295,34 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
             "psnr_note": "bug-compatible 1/Q dequantization for adaptive=0 (reference semantics)"}
 
 
+def movement_ceiling_leg(plan, luma, chroma, coef_y, coef_c, rounds=10):
+    """Same-box memory ceiling of the forward kernel's access pattern:
+    dctq_diag_movement_planes moves exactly the bytes of the multi-plane forward
+    launch (same grid, prefetch, LDS stage, 1 KiB non-temporal stores) with no
+    arithmetic.  Interleaved with the real launch, HIP events, medians.  Writes
+    pixel bytes into coef_y/coef_c: run after the parity check (later legs
+    recompute their own outputs)."""
+    import statistics
+    pls, outs = [luma, chroma], [coef_y, coef_c]
+    nblk = coef_y.shape[0] + coef_c.shape[0]
+    tk, tm = [], []
+    for r in range(rounds + 1):
+        for fn, acc in ((lambda: plan.forward_quant_planes(pls, outs=outs), tk),
+                        (lambda: plan.diag_movement_planes(pls, outs), tm)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                acc.append(e0.elapsed_time(e1) * 1e-3)
+    k, m = statistics.median(tk), statistics.median(tm)
+    ach = BYTES_PER_BLOCK * nblk / m / 1e9
+    return {"kernel": "fdct8_movement (dctq_diag_movement_planes: same bytes, no arithmetic)",
+            "achieved": ach, "frac": ach / HBM_PEAK_GBS, "median_us": m * 1e6,
+            "forward_median_us": k * 1e6, "forward_over_ceiling": m / k, "rounds": rounds}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -374,6 +404,9 @@ def main():
         except Exception as e:  # noqa: BLE001 -- report, do not hide
             parity = f"error: {e}"
 
+    movement = (movement_ceiling_leg(plan, luma, chroma, coef_y, coef_c, args.ceiling_rounds)
+                if args.ceiling_rounds > 0 else None)
+
     gather = None
     if world > 1 and args.gather_steps > 0:
         gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
@@ -422,7 +455,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": f"fdct8_quant_v2<{bool(args.adaptive)}, false, false>".lower(),
                          "avg_launch_us": avg_launch_s * 1e6, "launches_per_step": launches,
-                         "bytes_per_launch": avg_launch_bytes},
+                         "bytes_per_launch": avg_launch_bytes, "movement_ceiling": movement},
             "cpu_baseline": cpu,
             "parity_check": parity,
             "gather": gather,

@@ -48,6 +48,7 @@ def lib() -> C.CDLL:
             "dctq_forward_quant": ([vp, C.POINTER(_Plane), vp, vp, vp], i),
             "dctq_forward_quant_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_round_trip_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, vp], i),
+            "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_encode_workspace_bytes": ([ll], C.c_size_t),
             "dctq_encode_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, ll, vp, vp], i),
             "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
@@ -148,6 +149,15 @@ class Plan:
         _check(lib().dctq_forward_quant_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
                                                C.cast(vp, C.c_void_p) if vp is not None else None,
                                                _stream_ptr(stream)))
+        return outs
+
+    def diag_movement_planes(self, planes, outs, stream=None):
+        """DIAGNOSTIC: the bytes forward_quant_planes moves, with no arithmetic (outs receive
+        pixel bytes, not coefficients) -- the memory ceiling of that access pattern."""
+        n = len(planes)
+        descs = (_Plane * n)(*[plane_desc(px) for px in planes])
+        cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+        _check(lib().dctq_diag_movement_planes(self._h, descs, n, C.cast(cp, C.c_void_p), _stream_ptr(stream)))
         return outs
 
     def round_trip_planes(self, planes, outs=None, recons=None, var_nums=None, stream=None):

@@ -279,6 +279,17 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
     return DCTQ_OK;
 }
 
+int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                              void *stream) {
+    DCTQ_ENTRY;
+    if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
+    dctq::PlaneSet ps;
+    int rc = plane_set(planes, nplanes, coef, nullptr, &ps);
+    if (rc) return rc;
+    HIPCHK(dctq::launch_fdct8_movement(ps, (hipStream_t)stream, plan->num_cus), "fdct8_movement launch");
+    return DCTQ_OK;
+}
+
 int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                            int32_t *const *var_num, float *const *recon, void *stream) {
     DCTQ_ENTRY;

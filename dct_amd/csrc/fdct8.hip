@@ -432,4 +432,80 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
     if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
     DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring, ring_wgs));
 }
+// ============================================================================
+// Diagnostic: the v2 kernel's data movement with no arithmetic (the memory
+// ceiling of this exact access pattern, measured on the same box as the
+// kernel -- bench.py reports kernel time / this time).  Same persistent grid,
+// occupancy, prefetch, LDS stage, fence and 1 KiB non-temporal stores as
+// fdct8_batch; the "coefficients" are the pixel rows twice over.
+__global__ __launch_bounds__(kThreads, 4) void fdct8_movement(PlaneSet ps) {
+    __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ uint32_t qpad[kWaves * kQCap];   // same LDS footprint as fdct8_quant_v2
+    __shared__ uint16_t qpad2[kWaves * kQCap];  // (occupancy is LDS-bound)
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (ps.n < 0) { qpad[threadIdx.x] = 0; qpad2[threadIdx.x] = 0; }  // keep the padding allocated
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t step = gridDim.x * kWaves;
+    uint32_t g = blockIdx.x * kWaves + wv;
+    uint2 nxt[8];
+    {
+        const int k0 = plane_of(ps, g);
+        load_rows(ps.pl[k0], (g - ps.first[k0]) * 64 + lane, nxt);
+    }
+    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    for (; g < nbatch; g += step) {
+        const int k = plane_of(ps, g);
+        const PlaneArgs &p = ps.pl[k];
+        const uint32_t b = g - ps.first[k];
+        uint2 cur[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+        {
+            const uint32_t gn = g + step;
+            const int kn = plane_of(ps, gn);
+            load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
+        }
+        uint2 *mine = reinterpret_cast<uint2 *>(reinterpret_cast<char *>(stage) + (wv * 64 + lane) * kPitch2);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            mine[2 * r] = cur[r];
+            mine[2 * r + 1] = make_uint2(cur[r].y, cur[r].x);
+        }
+        asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                     "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t left = (uint32_t)p.nblk - b * 64;
+        const uint32_t nb = left < 64u ? left : 64u;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<char *>(coef_of(ps, k)) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+        const uint2 *st64 = reinterpret_cast<const uint2 *>(stage) + wv * 64 * (kPitch2 / 8);
+        u4v val[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int m = q * 64 + lane;
+            const int bl = m >> 3;
+            const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
+            val[q] = u4v{lo.x, lo.y, hi.x, hi.y};
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) __builtin_amdgcn_raw_buffer_store_b128(val[q], rs, lane * 16, q * 1024, DCTQ_STORE_AUX);
+    }
+}
+
+hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num_cus) {
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fdct8_movement, kThreads, 0) != hipSuccess || nb < 1) nb = 1;
+        per_cu = nb;
+    }
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
+    const uint32_t cap = (uint32_t)(num_cus * per_cu);
+    hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps);
+    return hipGetLastError();
+}
 }  // namespace dctq
