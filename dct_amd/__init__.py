@@ -63,6 +63,7 @@ def lib() -> C.CDLL:
             "dctq_rle_count": ([vp, ll, vp, vp, vp], i),
             "dctq_rle_emit": ([vp, ll, vp, vp, vp], i),
             "dctq_rle_decode": ([vp, vp, ll, vp, vp], i),
+            "dctq_huffman_bits": ([vp, ll, vp, vp], i),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -241,6 +242,18 @@ def rle_encode(coef, stream=None):
     _check(lib().dctq_rle_emit(C.c_void_p(coef.data_ptr()), n, C.c_void_p(off.data_ptr()),
                                C.c_void_p(sym.data_ptr()), s))
     return off, sym[:total]
+
+
+def huffman_bits(coef, out=None, stream=None):
+    """int16 [N, 64] quantized blocks -> int32 [N]: per block, the bits the reference's
+    get_encoded_size reports after build_huffman_codes on that block's RLE symbols
+    (tests/test_entropy.c:329-341)."""
+    import torch
+    n = coef.shape[0]
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=coef.device)
+    _check(lib().dctq_huffman_bits(C.c_void_p(coef.data_ptr()), n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    return out
 
 
 def rle_decode(symbols, offsets, out=None, stream=None):

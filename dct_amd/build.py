@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdct_amd.so")
-SOURCES = ["api.hip", "legacy.hip", "fdct8.hip", "fdct8_aux.hip", "f64_pair.hip", "rle.hip", "roundtrip.hip", "encode.hip"]
+SOURCES = ["api.hip", "legacy.hip", "fdct8.hip", "fdct8_aux.hip", "f64_pair.hip", "rle.hip", "roundtrip.hip", "encode.hip", "huffman.hip"]
 HEADERS = ["dctq_internal.h", "fdct8_bound.h", "host_tables.h", "aan_f64.h", "fdct8_core.h", "pair_core.h", "scan_core.h", "zigzag.h"]
 ARCH = "gfx950"
 

@@ -427,6 +427,16 @@ int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long 
     return DCTQ_OK;
 }
 
+int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, void *stream) {
+    DCTQ_ENTRY;
+    if (!coef || !bits) return fail(DCTQ_EINVAL, "coef/bits is NULL");
+    if (nblocks < 0) return fail(DCTQ_EINVAL, "nblocks < 0");
+    if (((uintptr_t)coef) % 16 || ((uintptr_t)bits) % 4) return fail(DCTQ_EINVAL, "coef must be 16-byte, bits 4-byte aligned");
+    if (nblocks == 0) return DCTQ_OK;
+    HIPCHK(dctq::launch_huffman_bits(coef, nblocks, bits, (hipStream_t)stream, device_cus()), "huffman_bits launch");
+    return DCTQ_OK;
+}
+
 int dctq_device_count(int *count) {
     DCTQ_ENTRY;
     HIPCHK(hipGetDeviceCount(count), "hipGetDeviceCount");

@@ -1,0 +1,166 @@
+// dct_amd/csrc/huffman.hip -- per-block Huffman size estimate on the GPU
+// (SURVEY 8(f)4): for every quantized block, the bit count the reference's
+// pipeline reports after coding that block on its own
+// (tests/test_entropy.c:329-341):
+//   run_length_encode (src/entropy.c:216-256) -> build_huffman_codes (:261-328)
+//   -> get_encoded_size (:363-399) = sum over symbols of (len(code) + 8).
+//
+// What is computed, and why it is exact:
+//  * The symbols of a block are its nonzero coefficients of zigzag positions
+//    0..62 plus the last element (7,7), zero or not (rle.hip).  Frequencies do
+//    not depend on order, so the multiset of symbol values is "every nonzero
+//    coefficient, plus a value 0 once if c[63] == 0" -- no zigzag needed.
+//  * build_huffman_codes merges the two minimum-frequency nodes of a binary heap
+//    until one is left (src/entropy.c:26-77 pops a true minimum every time), so
+//    its tree is a Huffman tree and sum(freq * depth) -- the code bits -- is the
+//    optimum, the same for every tie order.  A single distinct value is a lone
+//    leaf at depth 0 (code "", 0 bits).  Hence
+//        bits = 8 * count + WPL(frequencies)
+//    and WPL = the sum of the internal node weights of ANY Huffman merge order.
+//  * The GPU merges in weight buckets: cnt[w] = nodes of weight w.  Scanning w
+//    upward, the nodes of bucket w pair up among themselves (new weight 2w), an
+//    odd one left over waits as `pending` and merges with one node of the next
+//    non-empty bucket w' (new weight pending + w').  New weights are always above
+//    the current bucket, every merge takes the two smallest nodes, and weights
+//    never exceed count <= 64.
+// The oracle restates the reference's heap literally (oracle/dct_oracle.c,
+// orc_huffman_bits) and is pinned to the compiled reference; the GPU result is
+// compared with it (tests/test_gpu_parity.py::test_huffman_bits*).
+//
+// Layout: one LANE per block (64 blocks per wave).  The wave stages its tile
+// (8 KiB) in LDS with 1 KiB loads; each lane sorts its 64 values with a Batcher
+// odd-even merge network in registers (equal values become adjacent; zeros map
+// to the top and are dropped), adds one count per run length into its column
+// of an LDS histogram (16-bit counters, two lanes per dword, ds_add_u32), then
+// runs the bucket merge.  VALU-bound (~2000 instructions per 64 blocks).
+#include "dctq_internal.h"
+
+namespace dctq {
+
+constexpr int kHufWaves = 4;
+constexpr int kHufThreads = 64 * kHufWaves;
+constexpr int kHufPitch = 144;  // bytes per block in the tile stage (128 + 16: ds_read_b128 spread)
+
+__device__ __forceinline__ void cas(uint32_t &a, uint32_t &b) {
+    const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    a = lo;
+    b = hi;
+}
+
+// Batcher's odd-even merge sort of 64 registers (543 compare-exchanges), fully
+// unrolled so every index is a compile-time register.
+__device__ __forceinline__ void sort64(uint32_t (&a)[64]) {
+#pragma unroll
+    for (int p = 1; p < 64; p <<= 1)
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+            for (int j = k % p; j + k < 64; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; ++i)
+                    if (i + j + k < 64 && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cas(a[i + j], a[i + j + k]);
+}
+
+// Histogram column of `lane`: 16-bit counter of weight w (1..64) at byte
+// (w-1)*128 + lane*2 (dword (w-1)*32 + lane/2: lanes 2q, 2q+1 share a dword,
+// bank q -- conflict-free for any mix of weights across lanes).
+__device__ __forceinline__ void hist_add(char *h, int w, int lane, uint32_t n) {
+    __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(h + (w - 1) * 128 + (lane & ~1) * 2), n << (16 * (lane & 1)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+__global__ __launch_bounds__(kHufThreads) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
+                                                                   uint32_t *__restrict__ bits, long long ntiles) {
+    __shared__ uint4 lds[kHufWaves * 64 * kHufPitch / 16];  // per wave: tile stage, then the histogram (8 KiB)
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    char *mine = reinterpret_cast<char *>(lds) + wv * 64 * kHufPitch;
+    const long long stride = (long long)gridDim.x * kHufWaves;
+    for (long long t = (long long)blockIdx.x * kHufWaves + wv; t < ntiles; t += stride) {
+        const long long left = nblk - t * 64;
+        const int nb = left < 64 ? (int)left : 64;
+        // ---- tile -> LDS: load k covers blocks 8k..8k+7 (16 B per lane, 1 KiB per load)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int16_t *>(coef) + t * 64 * 64, (short)0, nb * 128, 0x00020000);  // past the tail: zeros
+        uint4 q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, 2 /* nt */);
+            q[k] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        // the previous tile's histogram reads are done (lgkmcnt) and its bits store
+        // retired with the loads above (one in-order vmcnt) before LDS is rewritten
+        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            *reinterpret_cast<uint4 *>(mine + (8 * k + (lane >> 3)) * kHufPitch + (lane & 7) * 16) = q[k];
+        __builtin_amdgcn_wave_barrier();
+        uint32_t a[64];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint4 w = *reinterpret_cast<const uint4 *>(mine + lane * kHufPitch + k * 16);
+            const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                // value*65536 - 1 as uint32: injective, and 0 -> 0xFFFFFFFF sorts last
+                a[8 * k + 2 * h] = (d[h] << 16) - 1u;
+                a[8 * k + 2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
+            }
+        }
+        const bool last_zero = a[63] == 0xFFFFFFFFu;  // c[63] == 0: value 0 is a symbol once
+        sort64(a);
+        // ---- runs of equal values -> histogram of frequencies
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile reads are done
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t count = last_zero ? 1u : 0u, nodes = count, run = 1;
+        if (last_zero) hist_add(mine, 1, lane, 1);
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            const bool real = a[i] != 0xFFFFFFFFu;
+            const bool end = real && (i == 63 || a[i + 1 < 64 ? i + 1 : 63] != a[i]);
+            if (end) hist_add(mine, run, lane, 1);
+            count += real ? 1u : 0u;
+            nodes += end ? 1u : 0u;
+            run = end ? 1u : run + 1u;
+        }
+        // ---- bucket merge (see the header): wpl = sum of internal node weights
+        uint32_t wpl = 0, pending = 0;
+        if (lane >= nb) nodes = 1;  // past the tail: nothing to do
+        for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
+            uint32_t c = *reinterpret_cast<const uint16_t *>(mine + (w - 1) * 128 + lane * 2);
+            if (nodes > 1) {
+                if (pending && c) {
+                    wpl += pending + w;
+                    hist_add(mine, pending + w, lane, 1);
+                    --c;
+                    --nodes;
+                    pending = 0;
+                }
+                const uint32_t pairs = c >> 1;
+                if (pairs) {
+                    wpl += pairs * 2 * w;
+                    nodes -= pairs;
+                    hist_add(mine, 2 * w, lane, pairs);
+                }
+                if (c & 1) pending = w;
+            }
+        }
+        const __amdgpu_buffer_rsrc_t rb =
+            __builtin_amdgcn_make_buffer_rsrc(bits + t * 64, (short)0, nb * 4, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(8u * count + wpl, rb, lane * 4, 0, 0);
+    }
+}
+
+hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bits, hipStream_t stream, int num_cus) {
+    const long long ntiles = (nblk + 63) / 64;
+    long long grid = (ntiles + kHufWaves - 1) / kHufWaves;
+    const long long cap = (long long)num_cus * 8;
+    if (grid > cap) grid = cap;
+    hipLaunchKernelGGL(huffman_bits_kernel, dim3((unsigned)grid), dim3(kHufThreads), 0, stream, coef, nblk, bits,
+                       ntiles);
+    return hipGetLastError();
+}
+}  // namespace dctq

@@ -142,6 +142,15 @@ int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offset
 int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
                     void *stream);
 
+/* Per-block Huffman size: bits[b] = what the reference's pipeline
+ * reports for block b coded on its own (tests/test_entropy.c:329-341):
+ * run_length_encode -> build_huffman_codes -> get_encoded_size
+ * (src/entropy.c:216-256, 261-328, 363-399), i.e. sum over the block's RLE
+ * symbols of (Huffman code length + 8).  The code lengths of one symbol depend
+ * on the reference heap's tie order, their sum does not (Huffman trees are
+ * optimal); the codes themselves are not produced.  coef 16-byte aligned. */
+int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, void *stream);
+
 /* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented
  * by the number of coefficients resolved by the exact fp64 tie path in later
  * dctq_forward_quant / _planes / dctq_round_trip_planes calls on this plan (costs one atomic per affected wave). */

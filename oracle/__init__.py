@@ -66,6 +66,9 @@ def _load_orc():
     lib.orc_rle_decode.argtypes = [C.c_int, _ip, _ip, C.c_int, _ip]
     lib.orc_rle_encode_plane.argtypes = [_i16p, C.c_long, C.c_void_p, C.c_void_p]
     lib.orc_rle_encode_plane.restype = C.c_long
+    lib.orc_huffman_bits.argtypes = [_ip]
+    lib.orc_huffman_bits.restype = C.c_int
+    lib.orc_huffman_bits_plane.argtypes = [_i16p, C.c_long, C.c_void_p]
     return lib
 
 
@@ -108,6 +111,8 @@ def ref():
         lib.ref_rle_decode.argtypes = [C.c_int, _ip, _ip, C.c_int, _ip]
         lib.ref_zigzag.argtypes = [C.c_int, _ip, _ip]
         lib.ref_forward_plane.restype = C.c_long
+        lib.ref_huffman_bits.argtypes = [C.c_int, _ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        lib.ref_huffman_bits.restype = C.c_int
         _ref = lib
     return _ref
 
@@ -253,3 +258,18 @@ def rle_encode_plane(coef: np.ndarray):
     sym = np.zeros(max(total, 1), np.uint32)
     orc().orc_rle_encode_plane(c, nblk, off.ctypes.data, sym.ctypes.data)
     return off, sym[:total]
+
+
+def huffman_bits(coeffs) -> int:
+    """One 8x8 int block -> the reference pipeline's per-block size: get_encoded_size after
+    build_huffman_codes on its RLE symbols (src/entropy.c:261-328, 363-399)."""
+    c = np.ascontiguousarray(coeffs, np.int32).reshape(64)
+    return int(orc().orc_huffman_bits(c))
+
+
+def huffman_bits_plane(coef: np.ndarray) -> np.ndarray:
+    """int16 [nblk, 64] -> uint32 [nblk] per-block Huffman sizes (huffman_bits of every block)."""
+    c = np.ascontiguousarray(coef, np.int16).reshape(-1, 64)
+    out = np.zeros(c.shape[0], np.uint32)
+    orc().orc_huffman_bits_plane(c, c.shape[0], out.ctypes.data)
+    return out

@@ -390,3 +390,90 @@ long orc_rle_encode_plane(const int16_t *coef, long nblk, uint32_t *offsets, uin
     if (offsets) offsets[nblk] = (uint32_t)total;
     return total;
 }
+
+/* ---- per-block Huffman size ------------------------------
+ * src/entropy.c:261-328 build_huffman_codes + :363-399 get_encoded_size for the
+ * symbols of one block, as the pipeline calls them (tests/test_entropy.c:
+ * 329-341, use_huffman = 1).  Restated with the reference's own heap
+ * discipline (pq_push :36-46 sifts up past strictly larger parents; pq_pop
+ * :48-77 moves the last node to the root and sifts down to the strictly
+ * smaller child, left first), leaves pushed in increasing symbol index
+ * (value + max|value| + 1), each merge popping left then right, so the tree --
+ * and every individual code length -- is the reference's. */
+typedef struct { unsigned freq; int value, left, right; } orc_hnode;
+
+static void orc_pq_push(int *heap, int *size, const orc_hnode *nodes, int node) {
+    int i = (*size)++;
+    while (i > 0 && nodes[heap[(i - 1) / 2]].freq > nodes[node].freq) {
+        heap[i] = heap[(i - 1) / 2];
+        i = (i - 1) / 2;
+    }
+    heap[i] = node;
+}
+
+static int orc_pq_pop(int *heap, int *size, const orc_hnode *nodes) {
+    int top = heap[0];
+    heap[0] = heap[--(*size)];
+    int i = 0;
+    while (i * 2 + 1 < *size) {
+        int s = i, l = 2 * i + 1, r = 2 * i + 2;
+        if (l < *size && nodes[heap[l]].freq < nodes[heap[s]].freq) s = l;
+        if (r < *size && nodes[heap[r]].freq < nodes[heap[s]].freq) s = r;
+        if (s == i) break;
+        int t = heap[i];
+        heap[i] = heap[s];
+        heap[s] = t;
+        i = s;
+    }
+    return top;
+}
+
+/* depth of every leaf (generate_codes :99-122: the code of a leaf is its path) */
+static void orc_depths(const orc_hnode *nodes, int node, int depth, int *len_of_value, int off) {
+    if (nodes[node].left < 0 && nodes[node].right < 0) {
+        len_of_value[nodes[node].value + off] = depth;
+        return;
+    }
+    if (nodes[node].left >= 0) orc_depths(nodes, nodes[node].left, depth + 1, len_of_value, off);
+    if (nodes[node].right >= 0) orc_depths(nodes, nodes[node].right, depth + 1, len_of_value, off);
+}
+
+int orc_huffman_bits(const int *coeffs) {
+    int v[64], r[64];
+    int cnt = orc_rle_encode(8, coeffs, v, r);
+    int maxs = 0;
+    for (int k = 0; k < cnt; ++k) maxs = abs(v[k]) > maxs ? abs(v[k]) : maxs;
+    int nsym = 2 * maxs + 2, off = maxs + 1;
+    unsigned *freq = (unsigned *)calloc((size_t)nsym, sizeof(unsigned));
+    int *len = (int *)calloc((size_t)nsym, sizeof(int));
+    orc_hnode *nodes = (orc_hnode *)malloc(sizeof(orc_hnode) * (size_t)(2 * nsym));
+    int *heap = (int *)malloc(sizeof(int) * (size_t)nsym);
+    for (int k = 0; k < cnt; ++k) freq[v[k] + off]++;
+    int nn = 0, size = 0;
+    for (int i = 0; i < nsym; ++i)
+        if (freq[i]) {
+            nodes[nn] = (orc_hnode){freq[i], i - off, -1, -1};
+            orc_pq_push(heap, &size, nodes, nn++);
+        }
+    while (size > 1) {
+        int a = orc_pq_pop(heap, &size, nodes), b = orc_pq_pop(heap, &size, nodes);
+        nodes[nn] = (orc_hnode){nodes[a].freq + nodes[b].freq, -1, a, b};
+        orc_pq_push(heap, &size, nodes, nn++);
+    }
+    orc_depths(nodes, orc_pq_pop(heap, &size, nodes), 0, len, off);
+    int bits = 0;
+    for (int k = 0; k < cnt; ++k) bits += len[v[k] + off] + 8;  /* code length + 8 run bits */
+    free(freq);
+    free(len);
+    free(nodes);
+    free(heap);
+    return bits;
+}
+
+void orc_huffman_bits_plane(const int16_t *coef, long nblk, uint32_t *bits) {
+    int c[64];
+    for (long b = 0; b < nblk; ++b) {
+        for (int k = 0; k < 64; ++k) c[k] = coef[b * 64 + k];
+        bits[b] = (uint32_t)orc_huffman_bits(c);
+    }
+}

@@ -27,5 +27,7 @@ void orc_zigzag_order(int n, int *order);
 int orc_rle_encode(int n, const int *coeffs, int *values, int *runs);
 void orc_rle_decode(int n, const int *values, const int *runs, int count, int *coeffs);
 long orc_rle_encode_plane(const int16_t *coef, long nblk, uint32_t *offsets, uint32_t *symbols);
+int orc_huffman_bits(const int *coeffs);
+void orc_huffman_bits_plane(const int16_t *coef, long nblk, uint32_t *bits);
 
 #endif

@@ -220,3 +220,21 @@ void ref_zigzag(int n, const int *coeffs, int *zz) {
     block_to_zigzag(b, zz, n);
     free_int_array(b, n);
 }
+
+/* The reference pipeline's per-block size (tests/test_entropy.c:329-341):
+ * run_length_encode -> build_huffman_codes -> get_encoded_size, use_huffman = 1.
+ * Also returns the block's Huffman code lengths by symbol value (for the
+ * fixtures; ties make individual lengths order-dependent, their sum is not). */
+int ref_huffman_bits(int n, const int *coeffs, int *nsym, int *ncodes) {
+    int **b = alloc_int_array(n, n);
+    for (int i = 0; i < n; ++i) memcpy(b[i], coeffs + i * n, sizeof(int) * n);
+    EntropyContext *e = entropy_init(1);
+    int cnt = run_length_encode(e, b, n);
+    build_huffman_codes(e);
+    int bits = get_encoded_size(e);
+    if (nsym) *nsym = cnt;
+    if (ncodes) *ncodes = e->huffman_size;
+    entropy_free(e);
+    free_int_array(b, n);
+    return bits;
+}

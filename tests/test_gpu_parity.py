@@ -600,6 +600,45 @@ def test_rle_large_planes(T, dm):
     assert np.array_equal(dm.rle_decode(sym, off).cpu().numpy(), c.cpu().numpy())
 
 
+def test_huffman_bits_golden_and_planes(T, dm):
+    """Per-block Huffman size on the GPU (huffman.hip: sort network + frequency histogram +
+    bucket merge) == the reference's get_encoded_size after build_huffman_codes
+    (tests/golden/huffman.json, made by the compiled reference) and == the oracle's literal
+    heap restatement on quantized planes of every input kind, ragged tile counts included."""
+    import json
+    import oracle as O
+    root = os.path.dirname(os.path.abspath(__file__))
+    g = json.load(open(os.path.join(root, "golden", "huffman.json")))
+    golden = np.array([b["coeffs"] for b in g["blocks"].values()], np.int16)
+    got = dm.huffman_bits(T.from_numpy(golden).cuda()).cpu().numpy().view(np.uint32)
+    assert got.tolist() == [b["bits"] for b in g["blocks"].values()]
+    rng = np.random.default_rng(21)
+    cases = [np.zeros((1, 64), np.int16), np.full((65, 64), -3, np.int16),
+             (rng.integers(-1024, 1025, (777, 64)) * (rng.random((777, 64)) < 0.5)).astype(np.int16)]
+    for kind, q, ad in [("uniform", 50, 0), ("smooth", 90, 1), ("const", 10, 0), ("extreme", 100, 0),
+                        ("uniform", 1, 1)]:
+        cases.append(O.forward_plane(O.synth_plane(7, O.KINDS[kind], 8 * 61, 8 * 9), q, ad))  # 549 blocks
+    for c in cases:
+        got = dm.huffman_bits(T.from_numpy(c).cuda()).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, O.huffman_bits_plane(c))
+
+
+def test_huffman_bits_large_plane(T, dm):
+    """A 4K luma frame stack (several tiles per wave in the grid-stride loop) + 5 ragged
+    blocks, every block against the oracle; invalid arguments rejected."""
+    import oracle as O
+    coef = dm.Plan(75, 0).forward_quant(dm.synth(41, "smooth", 3840, 2160, 2))
+    c = T.cat([coef, coef[:5]]).contiguous()
+    got = dm.huffman_bits(c).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, O.huffman_bits_plane(c.cpu().numpy()))
+    L = dm.lib()
+    out = T.empty(8, dtype=T.int32, device="cuda")
+    assert L.dctq_huffman_bits(None, 8, C.c_void_p(out.data_ptr()), None) == -1
+    assert L.dctq_huffman_bits(C.c_void_p(c.data_ptr() + 2), 8, C.c_void_p(out.data_ptr()), None) == -1
+    assert L.dctq_huffman_bits(C.c_void_p(c.data_ptr()), -1, C.c_void_p(out.data_ptr()), None) == -1
+    assert L.dctq_huffman_bits(C.c_void_p(c.data_ptr()), 0, C.c_void_p(out.data_ptr()), None) == 0
+
+
 def test_encode_planes_fused(T, dm):
     """dctq_encode_planes (forward + zigzag/RLE, the count fused into the forward) equals the
     oracle's run_length_encode of the oracle's quantized planes, blocks numbered plane

@@ -166,3 +166,70 @@ def test_rle_plane_format():
         r = s >> 16
         v2, r2 = O.rle_encode(coef[b].reshape(8, 8))
         assert v.tolist() == v2.tolist() and r.tolist() == r2.tolist()
+
+
+def _huffman_golden():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "huffman.json")))
+
+
+def bucket_merge_bits(block):
+    """Python model of the GPU's per-block Huffman size (dct_amd/csrc/huffman.hip):
+    frequencies of the symbol values (every nonzero coefficient, plus one 0 if
+    c[63] == 0), then the bucket merge: cnt[w] nodes of weight w, scanned upward,
+    pairs within a bucket, an odd node left pending for the next bucket.
+    bits = 8 * symbols + sum of internal node weights."""
+    c = np.asarray(block).ravel()
+    vals = [int(v) for v in c if v != 0] + ([0] if c[63] == 0 else [])
+    freq = {}
+    for v in vals:
+        freq[v] = freq.get(v, 0) + 1
+    cnt = [0] * 65
+    for f in freq.values():
+        cnt[f] += 1
+    nodes, wpl, pending = len(freq), 0, 0
+    for w in range(1, 65):
+        if nodes <= 1:
+            break
+        c_w = cnt[w]
+        if pending and c_w:
+            wpl += pending + w
+            cnt[pending + w] += 1
+            c_w -= 1
+            nodes -= 1
+            pending = 0
+        pairs = c_w // 2
+        if pairs:
+            wpl += pairs * 2 * w
+            nodes -= pairs
+            cnt[2 * w] += pairs
+        if c_w & 1:
+            pending = w
+    return 8 * len(vals) + wpl
+
+
+def test_huffman_oracle_vs_reference_golden():
+    """Per-block Huffman size (src/entropy.c:261-328 + 363-399 as tests/test_entropy.c:329-341
+    calls them): the oracle's literal restatement of the reference heap reproduces the
+    reference's own numbers (tests/golden/huffman.json)."""
+    g = _huffman_golden()
+    for name, b in g["blocks"].items():
+        assert O.huffman_bits(np.array(b["coeffs"])) == b["bits"], name
+    plane = np.array([b["coeffs"] for b in g["blocks"].values()], np.int16)
+    assert O.huffman_bits_plane(plane).tolist() == [b["bits"] for b in g["blocks"].values()]
+
+
+def test_huffman_bucket_model_is_exact():
+    """The GPU's bucket merge (tie-order free: a Huffman tree's weighted path length is the
+    optimum for every tie order) gives the reference's size on the golden blocks and on
+    random blocks of every density/amplitude against the oracle."""
+    g = _huffman_golden()
+    for name, b in g["blocks"].items():
+        assert bucket_merge_bits(b["coeffs"]) == b["bits"], name
+    rng = np.random.default_rng(99)
+    for k in range(3000):
+        dens = rng.random()
+        amp = int(rng.choice([1, 2, 3, 8, 100, 1024]))
+        blk = rng.integers(-amp, amp + 1, 64) * (rng.random(64) < dens)
+        assert bucket_merge_bits(blk) == O.huffman_bits(blk), blk.tolist()

@@ -50,6 +50,7 @@ for kind in ("uniform", "smooth"):
     off, sym = dct_amd.rle_encode(coef)
     total = sym.numel()
     back = torch.empty_like(coef)
+    hb = torch.empty(nblk, dtype=torch.int32, device="cuda")
     ws = torch.empty(int(dct_amd.lib().dctq_rle_workspace_bytes(nblk)) // 4 + 1, dtype=torch.int32, device="cuda")
     L = dct_amd.lib()
     import ctypes as C
@@ -59,6 +60,8 @@ for kind in ("uniform", "smooth"):
                                                C.c_void_p(ws.data_ptr()), s), nblk * (128 + 4 + 8)),
         "rle_emit": (lambda: L.dctq_rle_emit(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(off.data_ptr()),
                                              C.c_void_p(sym.data_ptr()), s), nblk * (128 + 4) + 4 * total),
+        "huffman_bits": (lambda: L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(hb.data_ptr()), s),
+                         nblk * (128 + 4)),
         "rle_decode": (lambda: L.dctq_rle_decode(C.c_void_p(sym.data_ptr()), C.c_void_p(off.data_ptr()), nblk,
                                                  C.c_void_p(back.data_ptr()), s), nblk * (128 + 4) + 4 * total),
     }

@@ -47,6 +47,7 @@ for step in "$@"; do
     planes) run planes 300 python tools/plane_bench.py ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
+    testhuf) run pytest_huf 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "huffman or rle" ;;
     enc) run enc 300 python tools/enc_bench.py ;;
     profenc) run profenc 600 rocprofv3 --kernel-trace --stats -d $OUT/profenc -o run --output-format csv -- python tools/enc_bench.py ;;
     profaux) run profaux 600 rocprofv3 --kernel-trace --stats -d $OUT/profaux -o run --output-format csv -- python tools/aux_bench.py ;;
