@@ -24,7 +24,10 @@ SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange.
 Also reported: the dominant kernel's roofline (algorithmic 192 B/block over the
 HIP-event-timed launch durations) and the reference's own CPU path
 (oracle/_ref/libref.so: src/dct.c + src/quantization.c compiled from
-/root/reference) timed on this host's cores in the same run.
+/root/reference) timed on this host's cores in the same run.  That CPU leg
+(cpu_leg, rank 0) is also where the oracle checks this run's GPU outputs (one
+chroma plane's coefficients and Huffman sizes): oracle/ is a checker here,
+never the thing measured.
 """
 from __future__ import annotations
 
@@ -102,6 +105,28 @@ def cpu_baseline(args):
                       f"adaptive={args.adaptive}) through ref_forward_plane: create_block_from_pixels -> "
                       f"dct_forward -> calculate_block_variance -> quantize per block, {threads} pthreads "
                       f"over block rows, {el:.1f} s"}
+
+
+def cpu_leg(args, world, fwd_check, huf_check):
+    """The CPU leg (rank 0): the reference's own CPU path timed on this host
+    (cpu_baseline, N=1 only), and the oracle as CHECKER of this run's GPU
+    outputs -- one chroma plane's coefficients and its per-block Huffman sizes.
+    The only part of bench.py that touches oracle/ (besides small_frame's
+    reference timing)."""
+    import numpy as np
+    import oracle as O
+    parity = {}
+    try:
+        if fwd_check is not None:
+            px, got = fwd_check
+            parity["forward"] = bool(np.array_equal(got, O.forward_plane(px, args.quality, args.adaptive, 8)))
+        if huf_check is not None:
+            c, b = huf_check
+            parity["huffman"] = bool(np.array_equal(b.view(np.uint32), O.huffman_bits_plane(c)))
+    except Exception as e:  # noqa: BLE001 -- report, do not hide
+        parity["error"] = str(e)
+    cpu = cpu_baseline(args) if world == 1 else None
+    return cpu, parity
 
 
 def gather_leg(args, plan, luma, coef_y, world, rank, dev):
@@ -221,6 +246,22 @@ def encode_leg(args, plan, luma, chroma, world, dev):
            "blocks_per_s": world * n * args.encode_steps / el, "ms_per_step": el / args.encode_steps * 1e3,
            "symbols_per_block": total / n, "stream_bytes_per_block": 4.0 * (1 + total / n),
            "coefficient_bytes_per_block": 128}
+    # the reference pipeline's per-block Huffman size (get_encoded_size after
+    # build_huffman_codes, tests/test_entropy.c:329-341) of every block just encoded
+    bits = [torch.empty(m, dtype=torch.int32, device=dev) for m in nbs]
+
+    def huffman():
+        for c, b in zip(coefs, bits):
+            dct_amd.huffman_bits(c, out=b)
+
+    el_h = timed(huffman)
+    mean_bits = float(sum(b.double().sum().item() for b in bits)) / n
+    k = 240 * 135  # first chroma plane: checked against the oracle in the CPU leg (cpu_leg)
+    huf_check = (coefs[1][:k].cpu().numpy(), bits[1][:k].cpu().numpy())
+    out["huffman"] = {"op": "huffman_bits (per-block Huffman size, reference get_encoded_size) over all planes",
+                      "blocks_per_s": world * n * args.encode_steps / el_h,
+                      "ms_per_step": el_h / args.encode_steps * 1e3, "bits_per_block": mean_bits,
+                      "compression_vs_u8": 512.0 / mean_bits, "_check": huf_check}
     if world > 1:
         def encode_gather():
             encode()
@@ -391,18 +432,12 @@ def main():
     avg_launch_bytes = BYTES_PER_BLOCK * (nblk_y + nblk_c) / launches
     achieved = avg_launch_bytes / avg_launch_s / 1e9
 
-    # quick parity self-check of the last step: one chroma plane vs the oracle
-    parity = None
+    # host copies of one chroma plane and its coefficients: the CPU leg (rank 0, N=1)
+    # checks them against the oracle
+    fwd_check = None
     if rank == 0:
-        try:
-            import numpy as np
-            import oracle as O
-            px = chroma[0].cpu().numpy()
-            want = O.forward_plane(px, args.quality, args.adaptive, 8)
-            got = coef_c[: want.shape[0]].cpu().numpy()
-            parity = bool(np.array_equal(got, want))
-        except Exception as e:  # noqa: BLE001 -- report, do not hide
-            parity = f"error: {e}"
+        nk = (C_W // 8) * (C_H // 8)
+        fwd_check = (chroma[0].cpu().numpy(), coef_c[:nk].cpu().numpy())
 
     movement = (movement_ceiling_leg(plan, luma, chroma, coef_y, coef_c, args.ceiling_rounds)
                 if args.ceiling_rounds > 0 else None)
@@ -433,7 +468,10 @@ def main():
         except Exception:
             traffic = None
     if rank == 0:
-        cpu = None if (args.no_cpu or world > 1) else cpu_baseline(args)  # rank 0 at N=1 only
+        huf_check = encode["huffman"].pop("_check", None) if encode else None
+        cpu, parity = (None, None) if args.no_cpu else cpu_leg(args, world, fwd_check, huf_check)
+        if encode and parity is not None:
+            encode["huffman"]["parity_check_chroma0"] = parity.get("huffman")
         out = {
             "metric": "8x8 macroblocks/sec (DCT+quant); % HBM roofline",
             "value": value,
@@ -457,7 +495,7 @@ def main():
                          "avg_launch_us": avg_launch_s * 1e6, "launches_per_step": launches,
                          "bytes_per_launch": avg_launch_bytes, "movement_ceiling": movement},
             "cpu_baseline": cpu,
-            "parity_check": parity,
+            "parity_check": parity.get("forward") if parity else None,
             "gather": gather,
             "round_trip": round_trip,
             "encode": encode,
