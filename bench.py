@@ -180,6 +180,30 @@ def small_frame_leg(args, plan, dev):
     el = time.perf_counter() - t0
     res = {"frame": "512x512 u8 (4096 blocks)", "launches": n, "us_per_frame": el / n * 1e6,
            "blocks_per_s": 4096 * n / el}
+    # the same launches captured once into a HIP graph and replayed (the host's
+    # per-call cost -- ctypes, argument checks, hipLaunchKernel -- paid at capture)
+    try:
+        per_graph, replays = 100, 4
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            plan.forward_quant(px, out=out)
+        torch.cuda.current_stream().wait_stream(side)
+        with torch.cuda.graph(g):
+            for _ in range(per_graph):
+                plan.forward_quant(px, out=out)
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(replays):
+            g.replay()
+        torch.cuda.synchronize()
+        elg = time.perf_counter() - t0
+        res.update({"graph_launches": per_graph * replays, "graph_us_per_frame": elg / (per_graph * replays) * 1e6,
+                    "graph_blocks_per_s": 4096 * per_graph * replays / elg})
+    except Exception as e:  # noqa: BLE001 -- report, do not hide
+        res["graph_error"] = str(e)
     host = px[0].cpu().numpy()
     got = out.cpu().numpy()
     if O.ref_available():
