@@ -1,10 +1,11 @@
 // dct_amd/csrc/legacy.hip -- the reference's per-block API (include/dct.h,
 // include/quantization.h, include/utils.h) as a drop-in, backed by the GPU.
 //
-// Each call marshals its row-pointer arrays into one staging buffer, runs a
-// small exact kernel that repeats the reference's fp64 arithmetic in the same
-// order (this file is compiled with -ffp-contract=off), and copies the result
-// back -- bit-identical to src/dct.c and src/quantization.c for any block size
+// Each call marshals its row-pointer arrays into one pinned, device-mapped
+// staging buffer, runs a small exact kernel that reads it over the host link,
+// repeats the reference's fp64 arithmetic in the same order (this file is
+// compiled with -ffp-contract=off) and writes the result back into it --
+// bit-identical to src/dct.c and src/quantization.c for any block size
 // up to 64.  It is a drop-in for callers that stay per-block; frame-level
 // callers should use include/dct_amd.h (one launch per plane).
 //
@@ -43,40 +44,44 @@ namespace {
 constexpr int kMaxN = 64;
 
 // ---------------------------------------------------------------- kernels
-// src/dct.c:52-77 -- one workgroup per block; temp in LDS.
-__global__ void k_forward(int n, const double *__restrict__ d, const double *__restrict__ in, double *__restrict__ out) {
-    extern __shared__ double tmp[];
-    const int nn = n * n;
-    for (int e = threadIdx.x; e < nn; e += blockDim.x) {
-        const int i = e / n, j = e % n;
-        double acc = 0.0;
-        for (int k = 0; k < n; ++k) acc += in[i * n + k] * d[j * n + k];  // input[i][k] * D^T[k][j]
-        tmp[e] = acc;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < nn; e += blockDim.x) {
-        const int i = e / n, j = e % n;
-        double acc = 0.0;
-        for (int k = 0; k < n; ++k) acc += d[i * n + k] * tmp[k * n + j];
-        out[e] = acc;
-    }
+// src/dct.c:52-77 (forward) and :80-105 (inverse) -- one workgroup per block.
+// `d` and `in` live in pinned host memory (zero-copy staging, see Staging): the
+// workgroup first copies them into LDS in one parallel round trip over the host
+// link (d stays in host memory when 3 n^2 doubles exceed kLdsTables), then runs
+// both passes from LDS and writes `out` straight back to host memory.
+constexpr int kLdsTables = 48 * 1024;
+__device__ __forceinline__ const double *stage_in(const double *__restrict__ src, double *dst, int nn) {
+    for (int e = threadIdx.x; e < nn; e += blockDim.x) dst[e] = src[e];
+    return dst;
 }
 
-// src/dct.c:80-105
-__global__ void k_inverse(int n, const double *__restrict__ d, const double *__restrict__ in, double *__restrict__ out) {
-    extern __shared__ double tmp[];
+template <bool FWD>
+__global__ void k_transform(int n, const double *__restrict__ dh, const double *__restrict__ inh,
+                            double *__restrict__ out) {
+    extern __shared__ double lds[];
     const int nn = n * n;
+    const bool dl = 3 * nn * (int)sizeof(double) <= kLdsTables;
+    double *tmp = lds, *in = lds + nn;
+    const double *d = dl ? stage_in(dh, lds + 2 * nn, nn) : dh;
+    stage_in(inh, in, nn);
+    __syncthreads();
     for (int e = threadIdx.x; e < nn; e += blockDim.x) {
         const int i = e / n, j = e % n;
         double acc = 0.0;
-        for (int k = 0; k < n; ++k) acc += d[k * n + i] * in[k * n + j];  // D^T[i][k] * input[k][j]
+        if (FWD)
+            for (int k = 0; k < n; ++k) acc += in[i * n + k] * d[j * n + k];  // input[i][k] * D^T[k][j]
+        else
+            for (int k = 0; k < n; ++k) acc += d[k * n + i] * in[k * n + j];  // D^T[i][k] * input[k][j]
         tmp[e] = acc;
     }
     __syncthreads();
     for (int e = threadIdx.x; e < nn; e += blockDim.x) {
         const int i = e / n, j = e % n;
         double acc = 0.0;
-        for (int k = 0; k < n; ++k) acc += tmp[i * n + k] * d[k * n + j];
+        if (FWD)
+            for (int k = 0; k < n; ++k) acc += d[i * n + k] * tmp[k * n + j];
+        else
+            for (int k = 0; k < n; ++k) acc += tmp[i * n + k] * d[k * n + j];
         out[e] = acc;
     }
 }
@@ -116,8 +121,13 @@ __global__ void k_elementwise(int mode, int nn, const double *__restrict__ m, in
     }
 }
 
-// src/quantization.c:153-169 -- sequential row-major sums (order matters for non-integer input).
-__global__ void k_variance(int nn, const double *__restrict__ x, double *__restrict__ out) {
+// src/quantization.c:153-169 -- sequential row-major sums (order matters for
+// non-integer input), after one parallel copy of the block into LDS.
+__global__ void k_variance(int nn, const double *__restrict__ xh, double *__restrict__ out) {
+    extern __shared__ double x[];
+    stage_in(xh, x, nn);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     double s = 0.0, s2 = 0.0;
     for (int k = 0; k < nn; ++k) {
         s += x[k];
@@ -128,21 +138,31 @@ __global__ void k_variance(int nn, const double *__restrict__ x, double *__restr
 }
 
 // ---------------------------------------------------------------- staging
+// Zero-copy: one pinned, device-mapped host buffer per thread.  A call packs its
+// row-pointer arrays into it, launches one kernel that reads its inputs from it
+// and writes its outputs back into it over the host link, and synchronizes: no
+// memcpy calls (each was a synchronous round trip through the driver).
 struct Staging {
-    void *dev = nullptr;
+    unsigned char *host = nullptr;  // pinned host memory
+    unsigned char *dev = nullptr;   // the same pages as seen by the device
     size_t bytes = 0;
-    std::vector<unsigned char> host;
-    void *get(size_t need) {
+    unsigned char *get(size_t need) {
         if (need > bytes) {
-            if (dev) (void)hipFree(dev);
-            LCHK(hipMalloc(&dev, need), "hipMalloc(legacy staging)");
+            if (host) (void)hipHostFree(host);
+            host = nullptr;
+            LCHK(hipHostMalloc((void **)&host, need, hipHostMallocMapped), "hipHostMalloc(legacy staging)");
+            LCHK(hipHostGetDevicePointer((void **)&dev, host, 0), "hipHostGetDevicePointer");
             bytes = need;
         }
-        if (host.size() < need) host.resize(need);
-        return dev;
+        return host;
     }
 };
 thread_local Staging g_stage;
+
+void finish(const char *what) {
+    LCHK(hipGetLastError(), what);
+    LCHK(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+}
 
 void pack(double **a, int n, double *dst) {
     for (int i = 0; i < n; ++i) memcpy(dst + i * n, a[i], sizeof(double) * n);
@@ -159,19 +179,17 @@ void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
     DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int n = ctx->block_size, nn = n * n;
     check_n(n);
-    const size_t bytes = sizeof(double) * 3 * nn;
-    double *dev = (double *)g_stage.get(bytes);
-    double *h = (double *)g_stage.host.data();
+    double *h = (double *)g_stage.get(sizeof(double) * 3 * nn);
+    const double *dv = (const double *)g_stage.dev;
     pack(ctx->dct_matrix, n, h);
     pack(input, n, h + nn);
-    LCHK(hipMemcpy(dev, h, sizeof(double) * 2 * nn, hipMemcpyHostToDevice), "hipMemcpy");
     const int threads = nn < 256 ? ((nn + 63) / 64) * 64 : 256;
+    const size_t lds = sizeof(double) * (3 * nn * sizeof(double) <= (size_t)kLdsTables ? 3 * nn : 2 * nn);
     if (fwd)
-        hipLaunchKernelGGL(k_forward, dim3(1), dim3(threads), sizeof(double) * nn, 0, n, dev, dev + nn, dev + 2 * nn);
+        hipLaunchKernelGGL(k_transform<true>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, (double *)dv + 2 * nn);
     else
-        hipLaunchKernelGGL(k_inverse, dim3(1), dim3(threads), sizeof(double) * nn, 0, n, dev, dev + nn, dev + 2 * nn);
-    LCHK(hipGetLastError(), "kernel launch");
-    LCHK(hipMemcpy(h + 2 * nn, dev + 2 * nn, sizeof(double) * nn, hipMemcpyDeviceToHost), "hipMemcpy");
+        hipLaunchKernelGGL(k_transform<false>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, (double *)dv + 2 * nn);
+    finish("transform launch");
     unpack(h + 2 * nn, n, output);
 }
 
@@ -181,20 +199,17 @@ void elementwise(int mode, int n, double **m, int flag, double variance, const d
     DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int nn = n * n;
     const size_t bytes = sizeof(double) * 3 * nn + sizeof(int) * 2 * nn;
-    unsigned char *dev = (unsigned char *)g_stage.get(bytes);
-    unsigned char *h = g_stage.host.data();
+    unsigned char *h = g_stage.get(bytes);
     double *hm = (double *)h, *hd = hm + nn;
     int *hi = (int *)(hd + 2 * nn);
     pack(m, n, hm);
     if (din) memcpy(hd, din, sizeof(double) * nn);
     if (iin) memcpy(hi, iin, sizeof(int) * nn);
-    LCHK(hipMemcpy(dev, h, bytes, hipMemcpyHostToDevice), "hipMemcpy");
-    double *dm = (double *)dev, *dd = dm + nn, *ddo = dd + nn;
+    double *dm = (double *)g_stage.dev, *dd = dm + nn, *ddo = dd + nn;
     int *di = (int *)(ddo + nn), *dio = di + nn;
     hipLaunchKernelGGL(k_elementwise, dim3((nn + 255) / 256), dim3(256), 0, 0, mode, nn, dm, flag, variance, dd, di,
                        ddo, dio);
-    LCHK(hipGetLastError(), "kernel launch");
-    LCHK(hipMemcpy(h, dev, bytes, hipMemcpyDeviceToHost), "hipMemcpy");
+    finish("elementwise launch");
     if (dout) memcpy(dout, (double *)h + 2 * nn, sizeof(double) * nn);
     if (iout) memcpy(iout, (int *)((double *)h + 3 * nn) + nn, sizeof(int) * nn);
 }
@@ -345,15 +360,13 @@ double calculate_block_variance(double **block, int block_size) {
     DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     check_n(block_size);
     const int nn = block_size * block_size;
-    double *dev = (double *)g_stage.get(sizeof(double) * (nn + 1));
-    double *h = (double *)g_stage.host.data();
+    double *h = (double *)g_stage.get(sizeof(double) * (nn + 1));
+    double *dv = (double *)g_stage.dev;
     pack(block, block_size, h);
-    LCHK(hipMemcpy(dev, h, sizeof(double) * nn, hipMemcpyHostToDevice), "hipMemcpy");
-    hipLaunchKernelGGL(k_variance, dim3(1), dim3(1), 0, 0, nn, dev, dev + nn);
-    LCHK(hipGetLastError(), "kernel launch");
-    double v = 0.0;
-    LCHK(hipMemcpy(&v, dev + nn, sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
-    return v;
+    const int threads = nn < 256 ? ((nn + 63) / 64) * 64 : 256;
+    hipLaunchKernelGGL(k_variance, dim3(1), dim3(threads), sizeof(double) * nn, 0, nn, dv, dv + nn);
+    finish("variance launch");
+    return h[nn];
 }
 
 double **adjust_matrix_for_block(QuantContext *ctx, double variance, int is_quantize) {
