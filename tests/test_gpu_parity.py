@@ -66,6 +66,24 @@ def test_forward_quant_full_size_digests(T, dm, digests):
         assert got == e["sha256"], e
 
 
+def test_bench_workload_every_block(T, dm):
+    """The bench's own step (64 4K luma + 128 1080p chroma planes in one dctq_forward_quant_planes launch,
+    12 441 600 blocks, bench.py's seeds) checked block by block against the oracle -- the headline number's
+    output, not a sample of it."""
+    import oracle as O
+    F = 64
+    luma = dm.synth(12345, "uniform", 3840, 2160, F)
+    chroma = dm.synth(12345 + 50000, "uniform", 1920, 1080, 2 * F)
+    cy, cc = dm.Plan(50, 0).forward_quant_planes([luma, chroma])
+    threads = min(16, os.cpu_count() or 1)
+    for px, coef, per in ((luma, cy, 480 * 270), (chroma, cc, 240 * 135)):
+        host_px = px.cpu().numpy()
+        host_c = coef.cpu().numpy()
+        for f in range(px.shape[0]):
+            want = O.forward_plane(host_px[f], 50, 0, threads)
+            assert np.array_equal(host_c[f * per:(f + 1) * per], want), f"frame {f} of {tuple(px.shape)}"
+
+
 def test_forward_quant_vs_oracle_many_seeds(T, dm):
     import oracle as O
     rng = np.random.default_rng(5)
