@@ -181,8 +181,8 @@ __global__ __launch_bounds__(kRleThreads) void rle_fixup_kernel(uint32_t *__rest
 // retires the previous tile's stores (store-data hazard); the next
 // tile's loads are in flight meanwhile.  Per block (~14 VALU): E = ballot(emit);
 // the symbol's index is mbcnt(E); its run is lane - 63 + clz64(((E << 1) | 1) &
-// lanes <= i), the sentinel bit 0 standing for "no earlier symbol".  Stores are
-// unconditional: lanes with nothing to store aim past num_records.
+// lanes <= i), the sentinel bit 0 standing for "no earlier symbol".  Only the
+// emitting lanes store (exec mask).
 __device__ __forceinline__ int tile_blocks(long long t, long long nblk) {
     const long long r = nblk - t * 64;
     return r < 0 ? 0 : r < 64 ? (int)r : 64;
@@ -259,8 +259,11 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
             const uint32_t idx =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(E >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)E, 0u));
             const uint32_t o = __builtin_amdgcn_readlane(offv, u);
-            const uint32_t addr = (emit && u < nb) ? (o - o0 + idx) * 4u : 0xFFFFFFF0u;  // dropped past num_records
-            __builtin_amdgcn_raw_buffer_store_b32(val | (runlen << 16), rsym, addr, 0, 0);
+            // exec-masked: only emitting lanes reach the addresser (-4 % dense, -6 % sparse
+            // against unconditional stores aimed past num_records, tools/rle_ab.py); the
+            // vmcnt(0) at the top of the next tile is explicit, so LLVM's waitcnt
+            // placement around predicated stores does not matter here
+            if (emit && u < nb) __builtin_amdgcn_raw_buffer_store_b32(val | (runlen << 16), rsym, (o - o0 + idx) * 4u, 0, 0);
         }
     }
 }

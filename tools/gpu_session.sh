@@ -46,6 +46,7 @@ for step in "$@"; do
     ceil4) run ceil4 180 tools/ubench/stream_ceiling4 ;;
     planes) run planes 300 python tools/plane_bench.py ;;
     legacy) run legacy 120 host/legacy_latency ;;
+    rleab) run rleab 300 python tools/rle_ab.py ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
     testhuf) run pytest_huf 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "huffman or rle" ;;

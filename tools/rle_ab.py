@@ -1,0 +1,54 @@
+"""A/B of dctq_rle_emit / dctq_rle_decode between the default libdct_amd.so and
+diagnostic builds (tools/ubench/libvar_*.so, tools/ubench/variant.sh), same inputs,
+interleaved, HIP events; outputs must match the default build.
+
+    python tools/rle_ab.py [frames]
+"""
+import ctypes as C
+import glob
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import dct_amd  # noqa: E402
+
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+W, H = 3840, 2160
+nblk = F * (W // 8) * (H // 8)
+libs = {"default": dct_amd.lib()}
+for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libvar_*.so"))):
+    L = C.CDLL(p)
+    L.dctq_rle_emit.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.dctq_rle_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p]
+    libs[os.path.basename(p)[7:-3]] = L
+s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+vp = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+for kind in ("uniform", "smooth"):
+    coef = dct_amd.Plan(50, 0).forward_quant(dct_amd.synth(9, kind, W, H, F))
+    off, sym = dct_amd.rle_encode(coef)
+    ref_sym = sym.clone()
+    outs = {k: torch.empty_like(sym) for k in libs}
+    backs = {k: torch.empty_like(coef) for k in libs}
+    jobs = {}
+    for k, L in libs.items():
+        jobs[f"emit {k}"] = lambda L=L, k=k: L.dctq_rle_emit(vp(coef), nblk, vp(off), vp(outs[k]), s)
+        jobs[f"decode {k}"] = lambda L=L, k=k: L.dctq_rle_decode(vp(sym), vp(off), nblk, vp(backs[k]), s)
+    times = {j: [] for j in jobs}
+    for r in range(9):
+        for j, fn in jobs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            assert fn() == 0
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                times[j].append(e0.elapsed_time(e1) * 1e-3)
+    for k in libs:
+        assert torch.equal(outs[k], ref_sym), f"{k}: emit output differs"
+        assert torch.equal(backs[k], coef), f"{k}: decode output differs"
+    for j, ts in times.items():
+        print(f"{kind:8s} {j:24s} median {statistics.median(ts) * 1e6:7.1f} us")
