@@ -25,6 +25,16 @@ class RandIsolation {
 #define DCTQ_ENTRY ::dctq::RandIsolation dctq_rand_isolation_
 
 
+// Resident workgroups per CU of `kernel` at `threads` per workgroup (>= 1).  The
+// launchers cache it in a function-local static (thread-safe initialisation):
+// every device this library runs on is a gfx950.
+template <typename K>
+inline int resident_per_cu(K kernel, int threads) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, 0) != hipSuccess || nb < 1) nb = 1;
+    return nb;
+}
+
 // n / d and n % d by multiply-high, valid for 0 <= n < 2^31 (host-built magic).
 struct FastDiv {
     uint32_t d, m, s;

@@ -86,9 +86,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
 
 template <typename K, typename... A>
 static hipError_t launch_enc(K kernel, uint32_t nbatch, int num_cus, hipStream_t stream, A... args) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess || per_cu < 1)
-        per_cu = 1;
+    const int per_cu = resident_per_cu(kernel, kThreads);
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
     const uint32_t cap = (uint32_t)(num_cus * per_cu);
     hipLaunchKernelGGL(kernel, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, args...);

@@ -211,9 +211,7 @@ __global__ __launch_bounds__(kThreadsP, 4) void idct8_pair(const DevTables *__re
 
 template <typename K, typename... A>
 static hipError_t launch_persistent(K kernel, long long nblk, int num_cus, hipStream_t stream, A... args) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreadsP, 0) != hipSuccess || per_cu < 1)
-        per_cu = 1;
+    const int per_cu = resident_per_cu(kernel, kThreadsP);
     const long long nbatch = (nblk + 31) / 32;
     const long long want = (nbatch + kWavesP - 1) / kWavesP;
     const long long cap = (long long)num_cus * per_cu;

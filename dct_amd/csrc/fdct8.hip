@@ -406,14 +406,7 @@ static hipError_t launch_v1(const PlaneSet &ps, const FastTables &t, const DevTa
 template <bool A, bool V, bool S>
 static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTables *dev, unsigned long long *fb,
                             hipStream_t stream, int num_cus, void *ring, int ring_wgs) {
-    static int per_cu = 0;  // resident workgroups per CU for this instantiation
-    if (per_cu == 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fdct8_quant_v2<A, V, S>, kThreads, 0) != hipSuccess ||
-            nb < 1)
-            nb = 1;
-        per_cu = nb;
-    }
+    static const int per_cu = resident_per_cu(fdct8_quant_v2<A, V, S>, kThreads);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
     uint32_t cap = (uint32_t)(num_cus * per_cu);
@@ -496,12 +489,7 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_movement(PlaneSet ps) {
 }
 
 hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num_cus) {
-    static int per_cu = 0;
-    if (per_cu == 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fdct8_movement, kThreads, 0) != hipSuccess || nb < 1) nb = 1;
-        per_cu = nb;
-    }
+    static const int per_cu = resident_per_cu(fdct8_movement, kThreads);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
     const uint32_t cap = (uint32_t)(num_cus * per_cu);

@@ -186,13 +186,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
 template <bool A, bool V, bool S>
 static hipError_t launch_rt(const RoundTripSet &rt, const DevTables *dev, unsigned long long *fb, hipStream_t stream,
                             int num_cus) {
-    static int per_cu = 0;
-    if (per_cu == 0) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, roundtrip8<A, V, S>, kThreads, 0) != hipSuccess || nb < 1)
-            nb = 1;
-        per_cu = nb;
-    }
+    static const int per_cu = resident_per_cu(roundtrip8<A, V, S>, kThreads);
     const uint32_t nbatch = rt.ps.first[rt.ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
     const uint32_t cap = (uint32_t)(num_cus * per_cu);
