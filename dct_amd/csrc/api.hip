@@ -242,6 +242,15 @@ int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter)
     return DCTQ_OK;
 }
 
+// A plan's tables and stash live on the device that was current at its creation.
+static int check_plan(const dctq_plan *plan) {
+    if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
+    int dev = -1;
+    HIPCHK(hipGetDevice(&dev), "hipGetDevice");
+    if (dev != plan->device) return fail(DCTQ_EINVAL, "plan was created on another device than the current one");
+    return DCTQ_OK;
+}
+
 static int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num,
                      dctq::PlaneSet *ps_out) {
     if (!planes || !coef) return fail(DCTQ_EINVAL, "planes/coef is NULL");
@@ -269,7 +278,7 @@ static int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef
 int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               int32_t *const *var_num, void *stream) {
     DCTQ_ENTRY;
-    if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
+    if (int rc = check_plan(plan)) return rc;
     dctq::PlaneSet ps;
     int rc = plane_set(planes, nplanes, coef, var_num, &ps);
     if (rc) return rc;
@@ -282,7 +291,7 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
 int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               void *stream) {
     DCTQ_ENTRY;
-    if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
+    if (int rc = check_plan(plan)) return rc;
     dctq::PlaneSet ps;
     int rc = plane_set(planes, nplanes, coef, nullptr, &ps);
     if (rc) return rc;
@@ -293,7 +302,8 @@ int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, i
 int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                            int32_t *const *var_num, float *const *recon, void *stream) {
     DCTQ_ENTRY;
-    if (!plan || !recon) return fail(DCTQ_EINVAL, "plan/recon is NULL");
+    if (int rc = check_plan(plan)) return rc;
+    if (!recon) return fail(DCTQ_EINVAL, "recon is NULL");
     dctq::RoundTripSet rt = {};
     int rc = plane_set(planes, nplanes, coef, var_num, &rt.ps);
     if (rc) return rc;
@@ -314,7 +324,8 @@ int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int npla
                        uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
                        void *stream) {
     DCTQ_ENTRY;
-    if (!plan || !offsets || !workspace) return fail(DCTQ_EINVAL, "plan/offsets/workspace is NULL");
+    if (int rc = check_plan(plan)) return rc;
+    if (!offsets || !workspace) return fail(DCTQ_EINVAL, "offsets/workspace is NULL");
     if (symbols_capacity < 0) return fail(DCTQ_EINVAL, "symbols_capacity < 0");
     dctq::EncodeSet es = {};
     int rc = plane_set(planes, nplanes, coef, nullptr, &es.ps);
@@ -341,7 +352,8 @@ int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *co
 
 int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream) {
     DCTQ_ENTRY;
-    if (!plan || !coef) return fail(DCTQ_EINVAL, "plan/coef is NULL");
+    if (int rc = check_plan(plan)) return rc;
+    if (!coef) return fail(DCTQ_EINVAL, "coef is NULL");
     if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
     dctq::PlaneArgs a;
     int rc = plane_args(src, &a);
@@ -357,7 +369,8 @@ int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef
 int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks, float *recon,
                  void *stream) {
     DCTQ_ENTRY;
-    if (!plan || !coef || !recon) return fail(DCTQ_EINVAL, "plan/coef/recon is NULL");
+    if (int rc = check_plan(plan)) return rc;
+    if (!coef || !recon) return fail(DCTQ_EINVAL, "coef/recon is NULL");
     if (plan->adaptive && !var_num) return fail(DCTQ_EINVAL, "adaptive inverse needs var_num");
     if (nblocks < 0 || nblocks >= (1ll << 40)) return fail(DCTQ_EINVAL, "bad nblocks");
     if (((uintptr_t)coef) % 16 || ((uintptr_t)recon) % 16) return fail(DCTQ_EINVAL, "coef/recon must be 16-byte aligned");
