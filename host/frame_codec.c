@@ -6,7 +6,8 @@
  * (tests/test_entropy.c:376-393 formula, clamped recon).  Then the same frame
  * through the fused round trip (dctq_round_trip_planes: must reproduce the
  * coefficients and the recon of the two calls) and the encoder
- * (dctq_encode_planes: run-length symbol count and an FNV-1a of the stream).
+ * (dctq_encode_planes: run-length symbol count and an FNV-1a of the stream),
+ * and the total of the per-block Huffman sizes (dctq_huffman_bits).
  *
  *   frame_codec WIDTH HEIGHT QUALITY ADAPTIVE SEED [KIND]
  */
@@ -108,6 +109,19 @@ int main(int argc, char **argv) {
     for (long long i = 0; i < (long long)total * 4; ++i) fs = (fs ^ sb[i]) * 1099511628211ULL;
     printf("symbols:%u\n", total);
     printf("symbols_fnv1a:%016llx\n", (unsigned long long)fs);
+
+    /* per-block Huffman size (the reference pipeline's get_encoded_size), summed */
+    void *bits;
+    CHK(dctq_malloc(&bits, (size_t)nblk * 4));
+    CHK(dctq_huffman_bits((const int16_t *)coef2, nblk, (uint32_t *)bits, NULL));
+    CHK(dctq_synchronize(NULL));
+    uint32_t *hb = malloc((size_t)nblk * 4);
+    CHK(dctq_memcpy_dtoh(hb, bits, (size_t)nblk * 4));
+    unsigned long long tb = 0;
+    for (long long i = 0; i < nblk; ++i) tb += hb[i];
+    printf("huffman_bits:%llu\n", tb);
+    dctq_free(bits);
+    free(hb);
     dctq_free(coef2);
     dctq_free(rec2);
     dctq_free(off);
