@@ -19,7 +19,9 @@ Another ("encode") runs the encoder (forward + zigzag run-length
 symbols) over the frames, and at N>1 the all-gather of the symbol streams.  At N>1 a
 second, separately reported leg ("gather") times forward DCT+quant of the luma frames followed by the RCCL
 all-gather of every rank's int16 coefficient planes (BASELINE configs[3],
-SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange.
+SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange; and "band"
+splits ONE 4K 4:2:0 frame across the ranks in block-row bands and all-gathers
+its coefficient planes (latency per frame).
 
 Also reported: the dominant kernel's roofline (algorithmic 192 B/block over the
 HIP-event-timed launch durations) and the reference's own CPU path
@@ -127,6 +129,53 @@ def cpu_leg(args, world, fwd_check, huf_check):
         parity["error"] = str(e)
     cpu = cpu_baseline(args) if world == 1 else None
     return cpu, parity
+
+
+def band_leg(args, plan, luma, chroma, world, dev, reps=20):
+    """N>1, the north_star's literal split: ONE 4K 4:2:0 frame (its Y, Cb and Cr
+    planes) partitioned across the ranks in block-row bands
+    (dct_amd.shard.band_shard), forward DCT+quant of every band in one
+    multi-plane launch, then the coefficient planes all-gathered so every rank
+    holds the whole frame's coefficients (three collectives, ragged bands
+    padded).  Latency-bound (194 400 blocks per frame); max-over-ranks wall
+    time per frame, and a check of the gathered planes against an unsharded
+    forward on this rank."""
+    from dct_amd import shard
+    # the same frame on every rank (each uses only its band of it)
+    y = dct_amd.synth(args.seed + 777, args.kind, luma.shape[-1], luma.shape[-2], 1, device=dev)
+    c = dct_amd.synth(args.seed + 778, args.kind, chroma.shape[-1], chroma.shape[-2], 2, device=dev)
+    planes = [y[0], c[0], c[1]]
+    bands, outs, counts = [], [], []
+    for p in planes:
+        band, (_, rows) = shard.band_shard(p, world, dist.get_rank())
+        bw = p.shape[-1] // 8
+        bands.append(band)
+        outs.append(torch.empty((rows * bw, 64), dtype=torch.int16, device=dev))
+        counts.append([(hi - lo) * bw for lo, hi in (shard.split(p.shape[-2] // 8, world, r) for r in range(world))])
+
+    def once():
+        plan.forward_quant_planes(bands, outs=outs)
+        return [shard.gather_coefficients(o, c) for o, c in zip(outs, counts)]
+
+    full = once()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        full = once()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    want = plan.forward_quant_planes(planes)
+    ok = all(bool(torch.equal(f, w)) for f, w in zip(full, want))
+    nblk = sum(w.shape[0] for w in want)
+    be = "RCCL all_gather_into_tensor" if dist.get_backend() == "nccl" else f"{dist.get_backend()} all_gather"
+    return {"op": f"one 4K 4:2:0 frame in block-row bands over {world} ranks: forward_quant_planes(bands) + {be} "
+                  "of the Y/Cb/Cr coefficient planes", "frames": reps, "us_per_frame": el / reps * 1e6,
+            "blocks_per_s": nblk * reps / el, "gathered_equals_unsharded": ok}
 
 
 def gather_leg(args, plan, luma, coef_y, world, rank, dev):
@@ -466,9 +515,10 @@ def main():
     movement = (movement_ceiling_leg(plan, luma, chroma, coef_y, coef_c, args.ceiling_rounds)
                 if args.ceiling_rounds > 0 else None)
 
-    gather = None
+    gather = band = None
     if world > 1 and args.gather_steps > 0:
         gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
+        band = band_leg(args, plan, luma, chroma, world, dev)
 
     small = small_frame_leg(args, plan, dev) if world == 1 and not args.no_cpu else None  # single-GPU config
 
@@ -521,6 +571,7 @@ def main():
             "cpu_baseline": cpu,
             "parity_check": parity.get("forward") if parity else None,
             "gather": gather,
+            "band": band,
             "round_trip": round_trip,
             "encode": encode,
             "small_frame": small,
