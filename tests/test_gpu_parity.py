@@ -66,22 +66,30 @@ def test_forward_quant_full_size_digests(T, dm, digests):
         assert got == e["sha256"], e
 
 
-def test_bench_workload_every_block(T, dm):
-    """The bench's own step (64 4K luma + 128 1080p chroma planes in one dctq_forward_quant_planes launch,
-    12 441 600 blocks, bench.py's seeds) checked block by block against the oracle -- the headline number's
-    output, not a sample of it."""
+@pytest.mark.parametrize("kind,q,ad,F", [("uniform", 50, 0, 64), ("smooth", 90, 1, 16), ("const", 75, 0, 16),
+                                         ("extreme", 10, 1, 8)])
+def test_bench_workload_every_block(T, dm, kind, q, ad, F):
+    """The bench's own step (F 4K luma + 2F 1080p chroma planes in one dctq_forward_quant_planes launch;
+    F = 64 is the headline 12 441 600 blocks with bench.py's seeds) checked block by block against the
+    oracle -- the headline number's output, not a sample of it -- plus other input kinds, qualities and the
+    adaptive mode at bench geometry, with var_num against the exact block variance numerator."""
     import oracle as O
-    F = 64
-    luma = dm.synth(12345, "uniform", 3840, 2160, F)
-    chroma = dm.synth(12345 + 50000, "uniform", 1920, 1080, 2 * F)
-    cy, cc = dm.Plan(50, 0).forward_quant_planes([luma, chroma])
+    luma = dm.synth(12345, kind, 3840, 2160, F)
+    chroma = dm.synth(12345 + 50000, kind, 1920, 1080, 2 * F)
+    ny, nc = F * 480 * 270, 2 * F * 240 * 135
+    vy = T.empty(ny, dtype=T.int32, device="cuda")
+    vc = T.empty(nc, dtype=T.int32, device="cuda")
+    cy, cc = dm.Plan(q, ad).forward_quant_planes([luma, chroma], var_nums=[vy, vc])
     threads = min(16, os.cpu_count() or 1)
-    for px, coef, per in ((luma, cy, 480 * 270), (chroma, cc, 240 * 135)):
+    for px, coef, vn, per in ((luma, cy, vy, 480 * 270), (chroma, cc, vc, 240 * 135)):
         host_px = px.cpu().numpy()
         host_c = coef.cpu().numpy()
+        host_v = vn.cpu().numpy()
         for f in range(px.shape[0]):
-            want = O.forward_plane(host_px[f], 50, 0, threads)
-            assert np.array_equal(host_c[f * per:(f + 1) * per], want), f"frame {f} of {tuple(px.shape)}"
+            want = O.forward_plane(host_px[f], q, ad, threads)
+            assert np.array_equal(host_c[f * per:(f + 1) * per], want), f"{kind}: frame {f} of {tuple(px.shape)}"
+        wv = O.plane_variance(host_px[-1]) * 4096.0  # var_num / 4096 == calculate_block_variance exactly
+        assert np.array_equal(host_v[-per:].astype(np.float64), wv), kind
 
 
 def test_forward_quant_vs_oracle_many_seeds(T, dm):
