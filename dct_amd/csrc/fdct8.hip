@@ -379,6 +379,7 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneSet ps, FastT
     for (; g < nbatch; g += step)
         fdct8_batch<ADAPTIVE, VAR, STATS>(ps, dev, fallbacks, stage, qb, qc, ring, qn, nxt, g, step, lane, wv);
     if (DCTQ_ABLATE & 16) qn = 0;
+    if (DCTQ_ABLATE & 2048) qn = 0;  // diagnostic: skip the final drain
     while (qn > 0) drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
 }
 

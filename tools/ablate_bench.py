@@ -16,7 +16,7 @@ libs = {"full": dct_amd.LIB_PATH}
 NAMES = {1: "no-tie-flags", 2: "no-butterfly", 8: "flags-no-queue", 16: "append-no-drain", 32: "queue-code-idle",
          64: "no-pixel-loads", 128: "no-coef-stores", 192: "no-loads-no-stores", 194: "no-mem-no-butterfly",
          256: "const-tables", 448: "const-tables-no-mem",
-         1024: "no-stash-stores", 1040: "no-stash-no-drain"}
+         1024: "no-stash-stores", 1040: "no-stash-no-drain", 2048: "no-final-drain"}
 for m, name in sorted(NAMES.items()):
     p = os.path.join(ROOT, "tools", "ubench", f"libablate_{m}.so")
     if os.path.exists(p):
