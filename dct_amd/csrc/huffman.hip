@@ -28,11 +28,13 @@
 // compared with it (tests/test_gpu_parity.py::test_huffman_bits*).
 //
 // Layout: one LANE per block (64 blocks per wave).  The wave stages its tile
-// (8 KiB) in LDS with 1 KiB loads; each lane sorts its 64 values with a Batcher
+// (8 KiB) in LDS with 1 KiB loads; each lane sorts its values with a Batcher
 // odd-even merge network in registers (equal values become adjacent; zeros map
-// to the top and are dropped), adds one count per run length into its column
-// of an LDS histogram (16-bit counters, two lanes per dword, ds_add_u32), then
-// runs the bucket merge.  VALU-bound (~2000 instructions per 64 blocks).
+// to the top and are dropped) -- all 64, or, when every block of the tile has
+// at most 16 / 32 nonzero coefficients (natural content), just those, compacted
+// through LDS -- adds one count per run length into its column of an LDS
+// histogram (16-bit counters, two lanes per dword, ds_add_u32), then runs the
+// bucket merge.  VALU-bound (~2000 instructions per 64 dense blocks).
 #include "dctq_internal.h"
 
 namespace dctq {
@@ -47,18 +49,19 @@ __device__ __forceinline__ void cas(uint32_t &a, uint32_t &b) {
     b = hi;
 }
 
-// Batcher's odd-even merge sort of 64 registers (543 compare-exchanges), fully
-// unrolled so every index is a compile-time register.
-__device__ __forceinline__ void sort64(uint32_t (&a)[64]) {
+// Batcher's odd-even merge sort of N registers (N = 16, 32, 64: 63, 191, 543
+// compare-exchanges), fully unrolled so every index is a compile-time register.
+template <int N>
+__device__ __forceinline__ void sort_net(uint32_t (&a)[N]) {
 #pragma unroll
-    for (int p = 1; p < 64; p <<= 1)
+    for (int p = 1; p < N; p <<= 1)
 #pragma unroll
         for (int k = p; k >= 1; k >>= 1)
 #pragma unroll
-            for (int j = k % p; j + k < 64; j += 2 * k)
+            for (int j = k % p; j + k < N; j += 2 * k)
 #pragma unroll
                 for (int i = 0; i < k; ++i)
-                    if (i + j + k < 64 && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cas(a[i + j], a[i + j + k]);
+                    if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cas(a[i + j], a[i + j + k]);
 }
 
 // Histogram column of `lane`: 16-bit counter of weight w (1..64) at byte
@@ -67,6 +70,102 @@ __device__ __forceinline__ void sort64(uint32_t (&a)[64]) {
 __device__ __forceinline__ void hist_add(char *h, int w, int lane, uint32_t n) {
     __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(h + (w - 1) * 128 + (lane & ~1) * 2), n << (16 * (lane & 1)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+constexpr uint32_t kSent = 0xFFFFFFFFu;  // a zero coefficient (dropped)
+
+// Sort key of coefficient i of a block held as 32 dwords (two int16 each):
+// value*65536 - 1 as uint32 -- injective, and 0 -> kSent, which sorts last.
+__device__ __forceinline__ uint32_t key_of(const uint32_t (&d)[32], int i) {
+    return ((i & 1) ? (d[i >> 1] & 0xFFFF0000u) : (d[i >> 1] << 16)) - 1u;
+}
+
+// Runs of equal values in the sorted registers -> one histogram count per
+// distinct value at its frequency; `count` += symbols, `nodes` += distinct values.
+template <int N>
+__device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine, int lane, uint32_t &count,
+                                             uint32_t &nodes) {
+    uint32_t run = 1;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool real = a[i] != kSent;
+        const bool end = real && (i == N - 1 || a[i + 1 < N ? i + 1 : N - 1] != a[i]);
+        if (end) hist_add(mine, run, lane, 1);
+        count += real ? 1u : 0u;
+        nodes += end ? 1u : 0u;
+        run = end ? 1u : run + 1u;
+    }
+}
+
+// Sparse waves (every block of the tile has <= N nonzero coefficients): the
+// nonzero values, compacted into the lane's LDS column (dword k*64 + lane:
+// conflict-free), come back as N registers padded with kSent and take the
+// N-network instead of the 64-one.
+// The lane's 64 coefficients from its row of the tile stage, as 32 dwords.
+__device__ __forceinline__ void tile_row(const char *mine, int lane, uint32_t (&d)[32]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(mine + lane * kHufPitch + k * 16);
+        d[4 * k] = w.x;
+        d[4 * k + 1] = w.y;
+        d[4 * k + 2] = w.z;
+        d[4 * k + 3] = w.w;
+    }
+}
+
+// Each path re-reads the tile row itself, so nothing but scalars is live across
+// the path choice and each path gets its own register allocation (a shared
+// 32-register row made the compiler hold 188-336 VGPRs).
+template <int N>
+__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &count, uint32_t &nodes) {
+    uint32_t d[32];
+    tile_row(mine, lane, d);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
+    __builtin_amdgcn_wave_barrier();
+    uint32_t pos = 0;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        const uint32_t v = key_of(d, i);
+        if (v != kSent) {
+            *reinterpret_cast<uint32_t *>(mine + (pos * 64 + lane) * 4) = v;
+            ++pos;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t b[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const uint32_t v = *reinterpret_cast<const uint32_t *>(mine + (k * 64 + lane) * 4);
+        b[k] = (uint32_t)k < pos ? v : kSent;
+    }
+    sort_net<N>(b);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): column reads done before the histogram overwrites them
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+    runs_to_hist<N>(b, mine, lane, count, nodes);
+}
+
+__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &count, uint32_t &nodes) {
+    uint32_t a[64];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint4 w = *reinterpret_cast<const uint4 *>(mine + lane * kHufPitch + k * 16);
+        const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            a[8 * k + 2 * h] = (d[h] << 16) - 1u;
+            a[8 * k + 2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
+        }
+    }
+    sort_net<64>(a);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile reads are done before the histogram overwrites them
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+    runs_to_hist<64>(a, mine, lane, count, nodes);
 }
 
 __global__ __launch_bounds__(kHufThreads) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
@@ -95,37 +194,27 @@ __global__ __launch_bounds__(kHufThreads) void huffman_bits_kernel(const int16_t
         for (int k = 0; k < 8; ++k)
             *reinterpret_cast<uint4 *>(mine + (8 * k + (lane >> 3)) * kHufPitch + (lane & 7) * 16) = q[k];
         __builtin_amdgcn_wave_barrier();
-        uint32_t a[64];
+        uint32_t nz = 0;
+        bool last_zero;  // c[63] == 0: value 0 is a symbol once
+        {
+            uint32_t d[32];
+            tile_row(mine, lane, d);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint4 w = *reinterpret_cast<const uint4 *>(mine + lane * kHufPitch + k * 16);
-            const uint32_t d[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-                // value*65536 - 1 as uint32: injective, and 0 -> 0xFFFFFFFF sorts last
-                a[8 * k + 2 * h] = (d[h] << 16) - 1u;
-                a[8 * k + 2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
-            }
+            for (int k = 0; k < 32; ++k) nz += ((d[k] & 0xFFFFu) != 0u) + ((d[k] >> 16) != 0u);
+            last_zero = (d[31] >> 16) == 0u;
         }
-        const bool last_zero = a[63] == 0xFFFFFFFFu;  // c[63] == 0: value 0 is a symbol once
-        sort64(a);
-        // ---- runs of equal values -> histogram of frequencies
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile reads are done
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
-        __builtin_amdgcn_wave_barrier();
-        uint32_t count = last_zero ? 1u : 0u, nodes = count, run = 1;
+        // the paths re-read the row: a memory clobber keeps the compiler from reusing
+        // (and holding) these 32 registers across the choice
+        asm volatile("" ::: "memory");
+        // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
+        uint32_t count = last_zero ? 1u : 0u, nodes = count;
+        if (!__builtin_amdgcn_ballot_w64(nz > 16))
+            sparse_runs<16>(mine, lane, count, nodes);
+        else if (!__builtin_amdgcn_ballot_w64(nz > 32))
+            sparse_runs<32>(mine, lane, count, nodes);
+        else
+            dense_runs(mine, lane, count, nodes);
         if (last_zero) hist_add(mine, 1, lane, 1);
-#pragma unroll
-        for (int i = 0; i < 64; ++i) {
-            const bool real = a[i] != 0xFFFFFFFFu;
-            const bool end = real && (i == 63 || a[i + 1 < 64 ? i + 1 : 63] != a[i]);
-            if (end) hist_add(mine, run, lane, 1);
-            count += real ? 1u : 0u;
-            nodes += end ? 1u : 0u;
-            run = end ? 1u : run + 1u;
-        }
         // ---- bucket merge (see the header): wpl = sum of internal node weights
         uint32_t wpl = 0, pending = 0;
         if (lane >= nb) nodes = 1;  // past the tail: nothing to do

@@ -643,6 +643,14 @@ def test_huffman_bits_golden_and_planes(T, dm):
     rng = np.random.default_rng(21)
     cases = [np.zeros((1, 64), np.int16), np.full((65, 64), -3, np.int16),
              (rng.integers(-1024, 1025, (777, 64)) * (rng.random((777, 64)) < 0.5)).astype(np.int16)]
+    # one tile per path of the kernel (every block <= 16 / <= 32 / some > 32 nonzero coefficients), with
+    # nonzeros at random positions (c[63] zero or not) and few distinct values (long runs, ties)
+    for lo, hi in [(0, 16), (17, 32), (30, 40), (16, 17), (32, 33)]:
+        blk = np.zeros((64, 64), np.int16)
+        for r in range(64):
+            k = int(rng.integers(lo, hi + 1))
+            blk[r, rng.choice(64, k, replace=False)] = rng.choice([-3, -1, 1, 2, 5, 300], k)
+        cases.append(blk)
     for kind, q, ad in [("uniform", 50, 0), ("smooth", 90, 1), ("const", 10, 0), ("extreme", 100, 0),
                         ("uniform", 1, 1)]:
         cases.append(O.forward_plane(O.synth_plane(7, O.KINDS[kind], 8 * 61, 8 * 9), q, ad))  # 549 blocks

@@ -1,0 +1,43 @@
+"""A/B of dctq_huffman_bits between the default libdct_amd.so and diagnostic
+builds (tools/ubench/libvar_*.so), same quantized planes (64 4K luma frames of
+each input kind, q50), interleaved, HIP events; outputs must match.
+
+    python tools/huf_ab.py [frames]
+"""
+import ctypes as C
+import glob
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import dct_amd  # noqa: E402
+
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+nblk = F * 480 * 270
+libs = {"default": dct_amd.lib()}
+for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libvar_*.so"))):
+    L = C.CDLL(p)
+    L.dctq_huffman_bits.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p]
+    libs[os.path.basename(p)[7:-3]] = L
+s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+for kind in ("uniform", "smooth", "const", "extreme"):
+    coef = dct_amd.Plan(50, 0).forward_quant(dct_amd.synth(9, kind, 3840, 2160, F))
+    outs = {k: torch.zeros(nblk, dtype=torch.int32, device="cuda") for k in libs}
+    times = {k: [] for k in libs}
+    for r in range(9):
+        for k, L in libs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            assert L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(outs[k].data_ptr()), s) == 0
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                times[k].append(e0.elapsed_time(e1) * 1e-3)
+    for k in libs:
+        assert torch.equal(outs[k], outs["default"]), f"{k} differs on {kind}"
+        med = statistics.median(times[k])
+        print(f"{kind:8s} {k:12s} median {med * 1e6:7.1f} us  {nblk / med / 1e9:6.2f} Gblk/s", flush=True)
