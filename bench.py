@@ -396,8 +396,17 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
     h, w = luma.shape[1], luma.shape[2]
     n0 = (h // 8) * (w // 8)
     orig = luma[0].reshape(h // 8, 8, w // 8, 8).permute(0, 2, 1, 3).reshape(n0, 64).double()
-    mse = float(((orig - rec[0][:n0].double().clamp(0, 255)) ** 2).mean())
-    psnr = float("inf") if mse == 0 else 10.0 * math.log10(255.0 * 255.0 / mse)
+
+    def psnr_of(r):
+        mse = float(((orig - r[:n0].double().clamp(0, 255)) ** 2).mean())
+        return float("inf") if mse == 0 else 10.0 * math.log10(255.0 * 255.0 / mse)
+
+    psnr = psnr_of(rec[0])
+    # the other dequantization semantics on the same frame: adaptive plans dequantize
+    # with Q (src/quantization.c:137,144), non-adaptive ones with the reference's 1/Q
+    other = dct_amd.Plan(args.quality, 0 if args.adaptive else 1)
+    (_,), (r_other,) = other.round_trip_planes([luma[0]])
+    psnr_other = psnr_of(r_other)
     bpb = 64 + 128 + 256
     return {"op": "round_trip_planes (fused forward+inverse, one launch per step)", "steps": args.round_trip_steps,
             "blocks_per_s": world * nblk * args.round_trip_steps / el,
@@ -406,7 +415,9 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
             "unfused_blocks_per_s": world * nblk * args.round_trip_steps / el_u,
             "unfused_bytes_per_block": 64 + 128 + 4 + 128 + 4 + 256,
             "psnr_db_luma_frame0": psnr,
-            "psnr_note": "bug-compatible 1/Q dequantization for adaptive=0 (reference semantics)"}
+            f"psnr_db_luma_frame0_adaptive{0 if args.adaptive else 1}": psnr_other,
+            "psnr_note": "adaptive=0 dequantizes with the reference's 1/Q (bug-compatible, src/quantization.c:139,144); "
+                         "adaptive=1 with Q*(2-nv)"}
 
 
 def movement_ceiling_leg(plan, luma, chroma, coef_y, coef_c, rounds=10):
