@@ -417,6 +417,77 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
     return hipGetLastError();
 }
 
+// ============================================================================
+// v3 (small launches): v2's loop with the flagged coefficients resolved IN
+// PLACE (the fused round trip's and the encoder's method, fdct8_core.h
+// resolve_ties) instead of the wave queue: after the prefetch fence, each lane
+// recomputes its own flagged coefficients in the reference's exact order from
+// the pixels still in its registers (tables from a 1 KiB LDS copy) and patches
+// the stage before the 1 KiB stores.  No stash, no drains, no patch stores.
+// On streams it is slower than v2 (divergent fp64 passes in ~78 % of batches,
+// DESIGN.md 3.1), but when every wave has at most one batch (a single frame:
+// 512x512 = 64 batches, 4K = 2 025) v2's end-of-kernel drain -- vmcnt(0), stash
+// loads, fp64, patch stores -- is the whole tail of the launch.
+template <bool ADAPTIVE, bool VAR, bool STATS>
+__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v3(PlaneSet ps, const DevTables *__restrict__ dev,
+                                                              unsigned long long *fallbacks) {
+    __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ ExactTables tab;
+    load_exact_tables(&tab, dev);
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t step = gridDim.x * kWaves;
+    uint32_t g = blockIdx.x * kWaves + wv;
+    uint2 nxt[8];
+    prefetch_batch(ps, g, lane, nxt);
+    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    uint32_t resolved = 0;
+    for (; g < nbatch; g += step) {
+        const int k = plane_of(ps, g);
+        const PlaneArgs &p = ps.pl[k];
+        const uint32_t b = g - ps.first[k];
+        uint2 cur[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+        prefetch_batch(ps, g + step, lane, nxt);
+        int32_t var_num;
+        uint32_t mlo, mhi;
+        forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)p.nblk, var_num, mlo,
+                                           mhi);
+        // the prefetch wait (retires the previous batch's stores too), then LDS reads
+        asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                     "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+        resolved += resolve_ties<ADAPTIVE>(&tab, cur, stage, lane, wv, mlo, mhi);
+        wave_sync();
+        u4v val[8];
+        stage_chunks(stage, wv, lane, val);
+        const uint32_t left = (uint32_t)p.nblk - b * 64;
+        const uint32_t nb = left < 64u ? left : 64u;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_STORE_AUX);
+        if (VAR) {
+            const __amdgpu_buffer_rsrc_t rv =
+                __builtin_amdgcn_make_buffer_rsrc(ps.var[k] + (size_t)b * 64, (short)0, (int)(nb * 4u), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_STORE_AUX);
+        }
+    }
+    if (STATS && resolved) atomicAdd(fallbacks, (unsigned long long)resolved);
+}
+
+template <bool A, bool V, bool S>
+static hipError_t launch_v3(const PlaneSet &ps, const DevTables *dev, unsigned long long *fb, hipStream_t stream,
+                            int num_cus) {
+    static const int per_cu = resident_per_cu(fdct8_quant_v3<A, V, S>, kThreads);
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
+    const uint32_t cap = (uint32_t)(num_cus * per_cu);
+    hipLaunchKernelGGL((fdct8_quant_v3<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps, dev, fb);
+    return hipGetLastError();
+}
+
 size_t fdct8_ring_bytes(int workgroups) { return (size_t)workgroups * kWaves * kQCap * 64; }
 
 hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
@@ -424,8 +495,13 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
                               int ring_wgs) {
     const bool a = adaptive != 0, v = ps.var[0] != nullptr, s = fallbacks != nullptr;
     if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
+    // at most one batch per wave of the resident grid: in-place ties (no drain tail)
+    const bool single = ps.first[ps.n] <= (uint32_t)ring_wgs * kWaves;
+    if (variant == 3 || (variant == 2 && single))  // variant 4: the queue kernel at any size (A/B)
+        DCTQ_SELECT(return launch_v3, a, v, s, (ps, dev, fallbacks, stream, num_cus));
     DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring, ring_wgs));
 }
+
 // ============================================================================
 // Diagnostic: the v2 kernel's data movement with no arithmetic (the memory
 // ceiling of this exact access pattern, measured on the same box as the
