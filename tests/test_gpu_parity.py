@@ -498,6 +498,27 @@ def test_legacy_transforms_bit_exact(L, blocks):
         L.dct_free(ctx)
 
 
+def test_legacy_large_blocks_and_variance(L):
+    """The per-block API at the sizes where the legacy kernels change staging (3 n^2 doubles above 48 KiB:
+    the DCT table is read from pinned host memory instead of LDS) up to the maximum n = 64, against the
+    oracle's restatement (bit-exact doubles); the variance of the same blocks (reference order)."""
+    import oracle as O
+    rng = np.random.default_rng(77)
+    for n in (32, 44, 45, 64):
+        ctx = L.dct_init(n)
+        x = rng.integers(-128, 128, (n, n)).astype(np.float64) + rng.random((n, n))
+        a, b, c = _put(L, x), L.alloc_array(n, n), L.alloc_array(n, n)
+        L.dct_forward(ctx, a, b)
+        assert (_get(b, n).view(np.uint64) == O.forward(x).view(np.uint64)).all(), n
+        L.dct_inverse(ctx, b, c)
+        assert (_get(c, n).view(np.uint64) == O.inverse(O.forward(x)).view(np.uint64)).all(), n
+        v = L.calculate_block_variance(a, n)
+        assert np.float64(v).view(np.uint64) == np.float64(O.variance(x)).view(np.uint64), n
+        for m in (a, b, c):
+            L.free_array(m, n)
+        L.dct_free(ctx)
+
+
 def test_legacy_quantization_bit_exact(L, blocks):
     from golden.make_golden import EXAMPLE
     c = f64(blocks["example_forward"]).reshape(8, 8)
