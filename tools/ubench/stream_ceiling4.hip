@@ -305,6 +305,97 @@ __global__ __launch_bounds__(256, 3) void kM16(const uint8_t *src, int bw, int n
     }
 }
 
+
+// v2 movement with the pixel rows of a batch CONTIGUOUS in memory (a tile-major
+// input layout the API does not have: load r = bytes [4096 b + 512 r, +512)):
+// does the 2-D row gather (8 rows 3840 B apart) cost anything?
+template <int AUX>
+__global__ __launch_bounds__(256, 4) void kMT(const uint8_t *src, int nblk, char *coef) {
+    __shared__ uint4 st[256 * 136 / 16];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nb = (nblk + 63) / 64;
+    char *ws = reinterpret_cast<char *>(st) + wv * 8704;
+    int b;
+    for (int it = 0; batch_of<0>(nb, it, b); ++it) {
+        const uint8_t *p = src + (size_t)b * 4096 + lane * 8;
+        uint2 r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { u2v t = __builtin_nontemporal_load((const u2v *)(p + k * 512)); r[k] = make_uint2(t.x, t.y); }
+        uint2 *mine = reinterpret_cast<uint2 *>(ws + lane * 136);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { mine[2 * k] = r[k]; mine[2 * k + 1] = make_uint2(r[k].x ^ 1, r[k].y); }
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __builtin_amdgcn_wave_barrier();
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(coef + (size_t)b * 8192, 0, 8192, 0x00020000);
+        u4v val[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            int m = k * 64 + lane, bl = m >> 3;
+            const uint2 *s2 = reinterpret_cast<const uint2 *>(ws + bl * 136 + (m & 7) * 16);
+            val[k] = u4v{s2[0].x, s2[0].y, s2[1].x, s2[1].y};
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rc, lane * 16, k * 1024, AUX);
+    }
+}
+
+// the inverse kernel's shape: 16-B contiguous loads of 8 KiB per 64 blocks (int16
+// coefficients), 16 KiB of 1 KiB stores (fp32): 1:2 like the forward, double the bytes
+template <int AUX>
+__global__ __launch_bounds__(256, 4) void kInv(const char *src, int nblk, char *dst) {
+    const int lane = threadIdx.x & 63;
+    const int nb = (nblk + 63) / 64;
+    int b;
+    for (int it = 0; batch_of<0>(nb, it, b); ++it) {
+        const u4v *p = reinterpret_cast<const u4v *>(src + (size_t)b * 8192) + lane;
+        u4v v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(p + k * 64);
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 16384, 0, 16384, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(u4v{v[k & 7][0] ^ k, v[k & 7][1], v[k & 7][2], v[k & 7][3]}, rc, lane * 16, k * 1024, AUX);
+    }
+}
+
+
+// the paired inverse kernel's data movement exactly (idct8_pair, no math): 32-block
+// batches, lane (h, j) loads rows 4h..4h+3 of block j (4 x 16 B, plain loads) of
+// the int16 coefficients, writes 128 B of its block's fp32 rows to the stage
+// (pitch 272), and the wave stores the stage as 8 x 1 KiB nt stores (8 KiB out)
+__global__ __launch_bounds__(256, 4) void kInvExact(const char *src, int nblk, char *dst) {
+    __shared__ uint4 st[4 * 32 * 272 / 16];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, j = lane & 31;
+    const int nb = (nblk + 31) / 32;
+    char *base = reinterpret_cast<char *>(st) + wv * 32 * 272;
+    int b;
+    for (int it = 0; batch_of<0>(nb, it, b); ++it) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(src + ((size_t)b * 32 + j) * 128) + 4 * h;
+        uint4 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = p[k];
+        char *mine = base + j * 272 + h * 128;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            *reinterpret_cast<uint4 *>(mine + k * 32) = r[k];
+            *reinterpret_cast<uint4 *>(mine + k * 32 + 16) = make_uint4(r[k].y, r[k].x, r[k].w, r[k].z);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        __builtin_amdgcn_wave_barrier();
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 32 * 256, 0, 8192, 0x00020000);
+        u4v val[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int bl = 4 * k + (lane >> 4);
+            const uint4 t = *reinterpret_cast<const uint4 *>(base + bl * 272 + (lane & 15) * 16);
+            val[k] = u4v{t.x, t.y, t.z, t.w};
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, 2);
+    }
+}
+
 // read-only sweep, 16 B/lane nt, 8 KiB per wave-iteration
 template <int MAP>
 __global__ __launch_bounds__(256) void kR(const char *src, int nchunk, unsigned *out) {
@@ -380,6 +471,16 @@ int main() {
     printf("--- same-box reference\n");
     TIME("M v2 movement nt/nt grid-stride", mb, hipLaunchKernelGGL((kM<2, 0, 1>), dim3(g4), dim3(256), 0, 0, src, bw, nblk, per, ls, lf, dst));
     TIME("W 8K nt    runs-of-4 16w/CU", wb, hipLaunchKernelGGL((kW<8, 2, 3>), dim3(g4), dim3(256), 0, 0, dst, nb));
+    TIME("MT tile-major contiguous input, 4 WG/CU", mb, hipLaunchKernelGGL((kMT<2>), dim3(g4), dim3(256), 0, 0, src, nblk, dst));
+    TIME("M v2 movement nt/nt grid-stride (again)", mb, hipLaunchKernelGGL((kM<2, 0, 1>), dim3(g4), dim3(256), 0, 0, src, bw, nblk, per, ls, lf, dst));
+    {   // inverse shape over 64 x 4K luma blocks: 128 B in (int16), 256 B out (fp32)
+        char *big; hipMalloc(&big, (size_t)nblk * 256 + (1 << 20));
+        TIME("Inv shape 16B loads 8K + 16K stores (384 B/blk)", (double)nblk * 384, hipLaunchKernelGGL((kInv<2>), dim3(g4), dim3(256), 0, 0, dst, nblk, big));
+        TIME("InvExact idct8_pair movement (384 B/blk)", (double)nblk * 384, hipLaunchKernelGGL(kInvExact, dim3(g4), dim3(256), 0, 0, dst, nblk, big));
+        TIME("M v2 movement nt/nt grid-stride (again)", mb, hipLaunchKernelGGL((kM<2, 0, 1>), dim3(g4), dim3(256), 0, 0, src, bw, nblk, per, ls, lf, dst));
+        TIME("InvExact idct8_pair movement (384 B/blk) again", (double)nblk * 384, hipLaunchKernelGGL(kInvExact, dim3(g4), dim3(256), 0, 0, dst, nblk, big));
+        hipFree(big);
+    }
     TIME("MG glds rows, 3 WG/CU", mb, hipLaunchKernelGGL((kMG<2, 3>), dim3(ncu * 3), dim3(256), 0, 0, src, bw, nblk, per, ls, lf, dst));
     TIME("MG glds rows, 2 WG/CU", mb, hipLaunchKernelGGL((kMG<2, 2>), dim3(ncu * 2), dim3(256), 0, 0, src, bw, nblk, per, ls, lf, dst));
     TIME("M16 16B reg rows via LDS, 3 WG/CU", mb, hipLaunchKernelGGL((kM16<2>), dim3(ncu * 3), dim3(256), 0, 0, src, bw, nblk, per, ls, lf, dst));
