@@ -280,14 +280,38 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
 // stores (store-data hazard); no store is issued inside the half.
 constexpr int kHalf = 32;
 
-__device__ __forceinline__ void decode_loads(const uint32_t *symbols, uint32_t offv, int g, int nb, int lane,
-                                             uint32_t (&sy)[kGroup], uint32_t (&cnt)[kGroup]) {
+// offv: lane b holds offsets[64t + b] (b < nb); oend = offsets[64t + nb], the end
+// of the tile's symbols (lane 64 does not exist, and readlane(64) would wrap).
+__device__ __forceinline__ uint32_t off_at(uint32_t offv, uint32_t oend, int b) {
+    return b < 64 ? __builtin_amdgcn_readlane(offv, b) : oend;
+}
+
+__device__ __forceinline__ void decode_loads(const uint32_t *symbols, uint32_t offv, uint32_t oend, int g, int nb,
+                                             int lane, uint32_t (&sy)[kGroup], uint32_t (&cnt)[kGroup]) {
 #pragma unroll
     for (int u = 0; u < kGroup; ++u) {
         const int jb = g + u < nb ? g + u : nb - 1;
-        const uint32_t o0 = __builtin_amdgcn_readlane(offv, jb), o1 = __builtin_amdgcn_readlane(offv, jb + 1);
+        const uint32_t o0 = __builtin_amdgcn_readlane(offv, jb), o1 = off_at(offv, oend, jb + 1);
         cnt[u] = g + u < nb ? o1 - o0 : 0u;
         sy[u] = (uint32_t)lane < cnt[u] ? symbols[o0 + lane] : 0u;
+    }
+}
+
+// Pair mode (every block of the half tile has <= 32 symbols: natural content):
+// lanes 0..31 hold block g+2u's symbols and lanes 32..63 block g+2u+1's, so
+// one load, one scan and one scatter serve two blocks.
+__device__ __forceinline__ void decode_loads_pair(const uint32_t *symbols, uint32_t offv, uint32_t oend, int g,
+                                                  int he, int lane, uint32_t (&sy)[kGroup], uint32_t (&cnt)[kGroup]) {
+    const int half = lane >> 5, s = lane & 31;
+#pragma unroll
+    for (int u = 0; u < kGroup; ++u) {
+        const int ba = g + 2 * u, bb = ba + 1;
+        const int ja = ba < he ? ba : he - 1, jb = bb < he ? bb : he - 1;
+        const uint32_t a0 = __builtin_amdgcn_readlane(offv, ja), a1 = off_at(offv, oend, ja + 1);
+        const uint32_t b0 = __builtin_amdgcn_readlane(offv, jb), b1 = off_at(offv, oend, jb + 1);
+        const uint32_t ca = ba < he ? a1 - a0 : 0u, cb = bb < he ? b1 - b0 : 0u;
+        cnt[u] = half ? cb : ca;
+        sy[u] = (uint32_t)s < cnt[u] ? symbols[(half ? b0 : a0) + s] : 0u;
     }
 }
 
@@ -304,17 +328,48 @@ __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t 
     for (long long t = (long long)blockIdx.x * kRleWaves + wv; t < ntiles; t += stride) {
         const long long b0 = t * 64;
         const int nb = tile_blocks(t, nblk);
-        const uint32_t offv = offsets[b0 + (lane < nb ? lane : nb)];  // lane nb: the end of the tile
+        const uint32_t offv = offsets[b0 + (lane < nb ? lane : nb)];  // lanes >= nb: the end of the tile
+        const uint32_t oend = offsets[b0 + nb];
+        // per-lane block symbol count (lane b: block b of the tile)
+        const uint32_t nxt_off = (uint32_t)__shfl_down((int)offv, 1);
+        const uint32_t cnt_lane = (lane == 63 ? oend : nxt_off) - offv;
         for (int h = 0; h < nb; h += kHalf) {
             const int he = nb < h + kHalf ? nb : h + kHalf;
+            const bool pair = !__builtin_amdgcn_ballot_w64(lane >= h && lane < he && cnt_lane > 32u);
             uint32_t sy[kGroup], cnt[kGroup];
-            decode_loads(symbols, offv, h, nb, lane, sy, cnt);
+            if (pair)
+                decode_loads_pair(symbols, offv, oend, h, he, lane, sy, cnt);
+            else
+                decode_loads(symbols, offv, oend, h, nb, lane, sy, cnt);
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the previous half's stores, before any LDS read
 #pragma unroll
             for (int k = 0; k < 4; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
+            if (pair) {
+                const int half = lane >> 5, s = lane & 31;
+                for (int g = h; g < he; g += 2 * kGroup) {
+                    uint32_t nsy[kGroup], ncnt[kGroup];
+                    decode_loads_pair(symbols, offv, oend, g + 2 * kGroup < he ? g + 2 * kGroup : g, he, lane, nsy, ncnt);
+#pragma unroll
+                    for (int u = 0; u < kGroup; ++u) {
+                        const bool live = (uint32_t)s < cnt[u];
+                        uint32_t e = wave_inclusive_scan(live ? (sy[u] >> 16) + 1u : 0u);
+                        const uint32_t lo = __builtin_amdgcn_readlane(e, 31);  // block A's total
+                        if (half) e -= lo;
+                        const uint32_t pos = e - 1u;
+                        const int b = g + 2 * u + half;
+                        if (live && pos < 64u && b < he)
+                            *reinterpret_cast<int16_t *>(lt + (b - h) * 128 + 2 * zz[pos]) = (int16_t)(sy[u] & 0xFFFFu);
+                    }
+#pragma unroll
+                    for (int u = 0; u < kGroup; ++u) {
+                        sy[u] = nsy[u];
+                        cnt[u] = ncnt[u];
+                    }
+                }
+            } else
             for (int g = h; g < he; g += kGroup) {
                 uint32_t nsy[kGroup], ncnt[kGroup];
-                decode_loads(symbols, offv, g + kGroup < he ? g + kGroup : g, nb, lane, nsy, ncnt);
+                decode_loads(symbols, offv, oend, g + kGroup < he ? g + kGroup : g, nb, lane, nsy, ncnt);
 #pragma unroll
                 for (int u = 0; u < kGroup; ++u) {
                     const uint32_t e = wave_inclusive_scan((uint32_t)lane < cnt[u] ? (sy[u] >> 16) + 1u : 0u);

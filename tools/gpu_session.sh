@@ -50,7 +50,7 @@ for step in "$@"; do
     hufab) run hufab 300 python tools/huf_ab.py ;;
     smallab) run smallab 300 python tools/small_ab.py ;;
     matrix) run matrix 300 python tools/perf_matrix.py ;;
-    ab23q) run ab23q 300 bash -c "python tools/ab_bench.py --variants 2,3 --rounds 12 && python tools/ab_bench.py --variants 2,3 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3 --rounds 6 --kind extreme --quality 10 && python tools/ab_bench.py --variants 2,3 --rounds 6 --adaptive 1" ;;
+    ab43) run ab43 300 bash -c "python tools/ab_bench.py --variants 4,3 --rounds 12 && python tools/ab_bench.py --variants 4,3 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 4,3 --rounds 6 --kind extreme --quality 10 && python tools/ab_bench.py --variants 4,3 --rounds 6 --adaptive 1" ;;
     clk) run clk 600 rocprofv3 --pmc GRBM_GUI_ACTIVE -d $OUT/pmc_clk -o run --output-format csv -- python tools/ablate_bench.py ;;
     aux) run aux 300 python tools/aux_bench.py ;;
     testhuf) run pytest_huf 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "huffman or rle" ;;
