@@ -26,18 +26,22 @@ for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libvar_*.so")))
 s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 for kind in ("uniform", "smooth", "const", "extreme"):
     coef = dct_amd.Plan(50, 0).forward_quant(dct_amd.synth(9, kind, 3840, 2160, F))
-    outs = {k: torch.zeros(nblk, dtype=torch.int32, device="cuda") for k in libs}
+    out = torch.zeros(nblk, dtype=torch.int32, device="cuda")  # shared by every build (see tools/rle_ab.py)
+    ref = None
     times = {k: [] for k in libs}
     for r in range(9):
         for k, L in libs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            assert L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(outs[k].data_ptr()), s) == 0
+            assert L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(out.data_ptr()), s) == 0
             e1.record()
             torch.cuda.synchronize()
             if r:
                 times[k].append(e0.elapsed_time(e1) * 1e-3)
+            elif ref is None:
+                ref = out.clone()
+            else:
+                assert torch.equal(out, ref), f"{k} differs on {kind}"
     for k in libs:
-        assert torch.equal(outs[k], outs["default"]), f"{k} differs on {kind}"
         med = statistics.median(times[k])
         print(f"{kind:8s} {k:12s} median {med * 1e6:7.1f} us  {nblk / med / 1e9:6.2f} Gblk/s", flush=True)
