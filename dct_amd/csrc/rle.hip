@@ -201,49 +201,123 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// zigzag position -> natural index as a compile-time table (register indexing
+// in the lane-per-block walk below must resolve statically)
+constexpr uint8_t kZzStatic[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                   12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                   35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                   58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+constexpr int kEmitPitch = 144;  // LDS bytes per block (128 + 16: lane-per-block row reads are conflict-free)
+constexpr int kEmitLds = 64 * kEmitPitch;
+#ifdef DCTQ_EMIT_WAVE_ONLY  // A/B switch (tools/rle_ab.py): every tile takes the wave-per-block path
+constexpr uint32_t kLaneWalkMax = 0;
+#else
+constexpr uint32_t kLaneWalkMax = 1024;  // symbols of a tile the lane-per-block path stages (<= kEmitLds / 4)
+#endif
+constexpr int kMaxChunks = 16;  // kLaneWalkMax / 64
+
+// A tile whose symbols fit the wave's LDS (natural content: ~6 symbols per
+// block) is walked lane-per-block: lane b reads block b's row, walks its 64
+// zigzag elements in registers (~6 VALU per element, no cross-lane work) and
+// writes its symbols at offsets[b] - offsets[64t] into LDS, which then leaves
+// as coalesced dword stores.  Denser tiles take the wave-per-block path.
+__device__ __forceinline__ void emit_lane_walk(const char *lt, char *ls, int lane, uint32_t base) {
+    uint32_t z[32];  // block `lane`, natural order, two elements per dword
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const u4r v = *reinterpret_cast<const u4r *>(lt + lane * kEmitPitch + 16 * k);
+        z[4 * k] = v[0], z[4 * k + 1] = v[1], z[4 * k + 2] = v[2], z[4 * k + 3] = v[3];
+    }
+    wave_sync_lds();  // every lane's row is in registers before the symbols overwrite the tile
+    // Branch-free: every element writes its would-be symbol at the block's next
+    // slot, which advances only past a nonzero -- a zero's write is overwritten
+    // by the next symbol (the last element always is one), so the slots
+    // [base, base + count) end up exactly the block's symbols.
+    uint32_t pos = base, run = 0;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        const int c = kZzStatic[i];
+        const uint32_t w = z[c >> 1];
+        const bool nz = (c & 1) ? w > 0xFFFFu : (w & 0xFFFFu) != 0u;
+        // (uint16)value | run << 16; the last element's run counts itself when zero
+        const uint32_t r = (i == 63 && !nz) ? run + 1u : run;
+        const uint32_t sym = __builtin_amdgcn_perm(r, w, (c & 1) ? 0x05040302u : 0x05040100u);
+        *reinterpret_cast<uint32_t *>(ls + pos * 4u) = sym;
+        pos += nz ? 1u : 0u;
+        run = nz ? 0u : run + 1u;
+    }
+}
+
 __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                const uint32_t *__restrict__ offsets,
                                                                uint32_t *__restrict__ symbols, long long ntiles,
                                                                unsigned long long capacity) {
-    __shared__ u4r tiles_lds[kRleWaves][64 * 8];
+    __shared__ u4r tiles_lds[kRleWaves][kEmitLds / 16];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const long long stride = (long long)gridDim.x * kRleWaves;
     const uint32_t zoff = 2u * kZigzag[lane];
     const uint64_t upto = ~0ull >> (63 - lane);  // lanes 0..lane
     const uint32_t upto_lo = (uint32_t)upto, upto_hi = (uint32_t)(upto >> 32);
+    const long long noffs = nblk + 1;  // offsets[nblk] = end of the last block's symbols
     const __amdgpu_buffer_rsrc_t roff = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t *>(offsets), (short)0, (int)(nblk * 4 < 0x7FFFFFFF ? nblk * 4 : 0x7FFFFFFF), 0x00020000);
+        const_cast<uint32_t *>(offsets), (short)0, (int)(noffs * 4 < 0x7FFFFFFF ? noffs * 4 : 0x7FFFFFFF), 0x00020000);
     long long t = (long long)blockIdx.x * kRleWaves + wv;
     if (t >= ntiles) return;
     u4r nq[8];
-    uint32_t noff;
+    uint32_t noff, nend;
     auto load_tile = [&](long long tt) {  // past the last tile: everything clipped, no traffic
-        const __amdgpu_buffer_rsrc_t rs = tile_rsrc(coef, tt, tile_blocks(tt, nblk));
+        const int nb = tile_blocks(tt, nblk);
+        const __amdgpu_buffer_rsrc_t rs = tile_rsrc(coef, tt, nb);
 #pragma unroll
         for (int k = 0; k < 8; ++k) nq[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, 2 /* nt */);
         noff = __builtin_amdgcn_raw_buffer_load_b32(roff, tt < ntiles ? (uint32_t)(tt * 64 + lane) * 4u : 0xFFFFFFF0u,
                                                     0, 0);
+        nend = __builtin_amdgcn_raw_buffer_load_b32(roff, tt < ntiles ? (uint32_t)(tt * 64 + nb) * 4u : 0xFFFFFFF0u,
+                                                    0, 0);
     };
     load_tile(t);
     char *lt = reinterpret_cast<char *>(tiles_lds[wv]);
+    // chunk k*64 + lane of the tile = block 8k + lane/8, bytes 16*(lane%8) of its row
+    const uint32_t wr = (uint32_t)(lane >> 3) * kEmitPitch + 16u * (lane & 7);
     for (; t < ntiles; t += stride) {
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this tile's loads and the previous tile's stores
         const uint32_t offv = noff;
+        const uint32_t o0 = __builtin_amdgcn_readlane(offv, 0);
+        const uint32_t nsym = __builtin_amdgcn_readfirstlane(nend) - o0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = nq[k];  // the tile's 8 KiB, in order
+        for (int k = 0; k < 8; ++k) *reinterpret_cast<u4r *>(lt + 8 * k * kEmitPitch + wr) = nq[k];
         load_tile(t + stride);
         wave_sync_lds();
-        uint32_t z[32];  // two blocks' elements per register (64 live VGPRs would halve the occupancy)
-#pragma unroll
-        for (int u = 0; u < 32; ++u)
-            z[u] = (uint32_t)*reinterpret_cast<const uint16_t *>(lt + 2 * u * 128 + zoff) |
-                   ((uint32_t)*reinterpret_cast<const uint16_t *>(lt + (2 * u + 1) * 128 + zoff) << 16);
         const int nb = tile_blocks(t, nblk);
         // the tile's symbols start at offsets[64t]: a per-tile descriptor keeps the
         // 32-bit voffset small (the stream itself may exceed 4 GiB); symbols at or
         // past `capacity` are dropped by num_records
-        const uint32_t o0 = __builtin_amdgcn_readlane(offv, 0);
         const unsigned long long room = capacity > o0 ? capacity - o0 : 0ull;
+        if (nsym <= kLaneWalkMax) {
+            if (lane < nb) emit_lane_walk(lt, lt, lane, offv - o0);
+            wave_sync_lds();
+            const uint32_t nrec = (uint32_t)(room < nsym ? room : nsym) * 4u;
+            const __amdgpu_buffer_rsrc_t rsym =
+                __builtin_amdgcn_make_buffer_rsrc(symbols + o0, (short)0, (int)nrec, 0x00020000);
+            // all LDS reads first, then the stores (store-data hazard); chunks
+            // of 64 symbols in guarded groups of 4, the tail clipped by num_records
+            uint32_t v[kMaxChunks];
+#pragma unroll
+            for (int j = 0; j < kMaxChunks; ++j) v[j] = *reinterpret_cast<const uint32_t *>(lt + (j * 64 + lane) * 4);
+#pragma unroll
+            for (int g = 0; g < kMaxChunks; g += 4)
+                if (g * 64 < (int)nsym) {
+#pragma unroll
+                    for (int j = g; j < g + 4; ++j)
+                        __builtin_amdgcn_raw_buffer_store_b32(v[j], rsym, (j * 64 + lane) * 4, 0, 0);
+                }
+            continue;
+        }
+        uint32_t z[32];  // two blocks' elements per register (64 live VGPRs would halve the occupancy)
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+            z[u] = (uint32_t)*reinterpret_cast<const uint16_t *>(lt + 2 * u * kEmitPitch + zoff) |
+                   ((uint32_t)*reinterpret_cast<const uint16_t *>(lt + (2 * u + 1) * kEmitPitch + zoff) << 16);
         const __amdgpu_buffer_rsrc_t rsym = __builtin_amdgcn_make_buffer_rsrc(
             symbols + o0, (short)0, (int)((room < 4096ull ? room : 4096ull) * 4u), 0x00020000);
 #pragma unroll

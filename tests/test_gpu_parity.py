@@ -619,6 +619,15 @@ def test_rle_bit_exact_and_round_trip(T, dm):
     px = O.synth_plane(4, O.KINDS["smooth"], 640, 480)
     cases.append(O.forward_plane(px, 75, 0))          # real quantized planes: ragged tiles (4800 blocks)
     cases.append(O.forward_plane(O.synth_plane(5, 0, 512, 256), 90, 1))
+
+    def blocks_with(counts):  # block i has counts[i] symbols: counts[i]-1 nonzeros off (7,7), (7,7) zero
+        b = np.zeros((len(counts), 64), np.int16)
+        for i, k in enumerate(counts):
+            b[i, rng.permutation(63)[:k - 1]] = rng.integers(1, 300, k - 1) * rng.choice([-1, 1], k - 1)
+        return b
+    # emit's two paths (rle.hip): tiles of <= 1024 symbols go lane-per-block through LDS, denser
+    # ones wave-per-block -- tiles at 1024 / 1025 symbols, alternating tiles, a ragged sparse tail
+    cases.append(blocks_with([16] * 64 + [16] * 63 + [17] + [1] * 64 + [64] * 64 + [2] * 64 + [40] * 64 + [3] * 29))
     for c in cases:
         off, sym = dm.rle_encode(T.from_numpy(c).cuda())
         woff, wsym = O.rle_encode_plane(c)

@@ -27,8 +27,9 @@ for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libvar_*.so")))
     libs[os.path.basename(p)[7:-3]] = L
 s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 vp = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
-for kind in ("uniform", "smooth"):
-    coef = dct_amd.Plan(50, 0).forward_quant(dct_amd.synth(9, kind, W, H, F))
+for kind, q in (("uniform", 50), ("smooth", 50), ("smooth", 90), ("const", 50), ("extreme", 50)):
+    coef = dct_amd.Plan(q, 0).forward_quant(dct_amd.synth(9, kind, W, H, F))
+    kind = f"{kind}/q{q}"
     off, sym = dct_amd.rle_encode(coef)
     ref_sym = sym.clone()
     # ONE output buffer per operation, shared by every build: separate buffers put
@@ -55,4 +56,4 @@ for kind in ("uniform", "smooth"):
                 else:
                     assert torch.equal(back, coef), f"{k}: decode output differs"
     for j, ts in times.items():
-        print(f"{kind:8s} {j:24s} median {statistics.median(ts) * 1e6:7.1f} us")
+        print(f"{kind:12s} {j:24s} median {statistics.median(ts) * 1e6:7.1f} us")
