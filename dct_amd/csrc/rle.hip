@@ -209,7 +209,7 @@ constexpr uint8_t kZzStatic[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 2
                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 constexpr int kEmitPitch = 144;  // LDS bytes per block (128 + 16: lane-per-block row reads are conflict-free)
 constexpr int kEmitLds = 64 * kEmitPitch;
-#ifdef DCTQ_EMIT_WAVE_ONLY  // A/B switch (tools/rle_ab.py): every tile takes the wave-per-block path
+#ifdef DCTQ_RLE_WAVE_ONLY  // A/B switch (tools/rle_ab.py): every emit/decode tile takes the wave-per-block path
 constexpr uint32_t kLaneWalkMax = 0;
 #else
 constexpr uint32_t kLaneWalkMax = 1024;  // symbols of a tile the lane-per-block path stages (<= kEmitLds / 4)
@@ -389,16 +389,30 @@ __device__ __forceinline__ void decode_loads_pair(const uint32_t *symbols, uint3
     }
 }
 
+// Lane path (a half tile of at most kDecLaneMax symbols: natural content):
+// the half's symbols come in as coalesced dword loads and go to LDS behind the
+// zeroed half tile, and lane i < 32 walks block h+i's symbols
+// (pos += run; tile[i][zigzag[pos]] = value while pos < 64; pos++) -- about 6
+// instructions per symbol per lane instead of a scan and scatter per block.
+// 4 KiB + 960 B per wave keeps 8 waves/SIMD (the dense path needs them).
+#ifdef DCTQ_RLE_WAVE_ONLY
+constexpr uint32_t kDecLaneMax = 0;
+#else
+constexpr uint32_t kDecLaneMax = 240;
+#endif
+constexpr int kDecLds = kHalf * 128 + 240 * 4;
+
 __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t *__restrict__ symbols,
                                                                  const uint32_t *__restrict__ offsets, long long nblk,
                                                                  int16_t *__restrict__ coef, long long ntiles) {
-    __shared__ u4r half_lds[kRleWaves][kHalf * 8];
+    __shared__ u4r wave_lds[kRleWaves][kDecLds / 16];
     __shared__ uint8_t zz[64];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < 64) zz[threadIdx.x] = kZigzag[threadIdx.x];
     __syncthreads();
     const long long stride = (long long)gridDim.x * kRleWaves;
-    char *lt = reinterpret_cast<char *>(half_lds[wv]);
+    char *lt = reinterpret_cast<char *>(wave_lds[wv]);
+    uint32_t *lsym = reinterpret_cast<uint32_t *>(lt + kHalf * 128);
     for (long long t = (long long)blockIdx.x * kRleWaves + wv; t < ntiles; t += stride) {
         const long long b0 = t * 64;
         const int nb = tile_blocks(t, nblk);
@@ -409,53 +423,90 @@ __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t 
         const uint32_t cnt_lane = (lane == 63 ? oend : nxt_off) - offv;
         for (int h = 0; h < nb; h += kHalf) {
             const int he = nb < h + kHalf ? nb : h + kHalf;
-            const bool pair = !__builtin_amdgcn_ballot_w64(lane >= h && lane < he && cnt_lane > 32u);
-            uint32_t sy[kGroup], cnt[kGroup];
-            if (pair)
-                decode_loads_pair(symbols, offv, oend, h, he, lane, sy, cnt);
-            else
-                decode_loads(symbols, offv, oend, h, nb, lane, sy, cnt);
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the previous half's stores, before any LDS read
+            const uint32_t s0 = __builtin_amdgcn_readlane(offv, h), nh = off_at(offv, oend, he) - s0;
+            if (kDecLaneMax && nh <= kDecLaneMax) {
+                const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
+                uint32_t v[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
-            if (pair) {
-                const int half = lane >> 5, s = lane & 31;
-                for (int g = h; g < he; g += 2 * kGroup) {
-                    uint32_t nsy[kGroup], ncnt[kGroup];
-                    decode_loads_pair(symbols, offv, oend, g + 2 * kGroup < he ? g + 2 * kGroup : g, he, lane, nsy, ncnt);
+                for (int j = 0; j < 4; ++j)  // past nh: clipped to 0, no traffic
+                    v[j] = __builtin_amdgcn_raw_buffer_load_b32(rsy, (j * 64 + lane) * 4, 0, 0);
+                // block h+i's start and count, to lane i
+                const uint32_t my_off = (uint32_t)__shfl((int)offv, (lane + h) & 63);
+                const uint32_t my_cnt = (uint32_t)__shfl((int)cnt_lane, (lane + h) & 63);
+                // vmcnt(0): these loads, and the previous half's stores before any LDS read (store-data hazard)
+                __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
-                    for (int u = 0; u < kGroup; ++u) {
-                        const bool live = (uint32_t)s < cnt[u];
-                        uint32_t e = wave_inclusive_scan(live ? (sy[u] >> 16) + 1u : 0u);
-                        const uint32_t lo = __builtin_amdgcn_readlane(e, 31);  // block A's total
-                        if (half) e -= lo;
-                        const uint32_t pos = e - 1u;
-                        const int b = g + 2 * u + half;
-                        if (live && pos < 64u && b < he)
-                            *reinterpret_cast<int16_t *>(lt + (b - h) * 128 + 2 * zz[pos]) = (int16_t)(sy[u] & 0xFFFFu);
+                for (int j = 0; j < 4; ++j)
+                    if (j < 3 || lane < 48) lsym[j * 64 + lane] = v[j];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
+                wave_sync_lds();
+                // a block's symbols must lie inside the half's (bounds the walk for any offsets)
+                const uint32_t base = my_off - s0;
+                const uint32_t cnt =
+                    lane < he - h && base <= nh ? (my_cnt < nh - base ? my_cnt : nh - base) : 0u;
+                int16_t *row = reinterpret_cast<int16_t *>(lt + (lane & 31) * 128);
+                uint32_t pos = 0;
+                for (uint32_t i = 0; i < cnt; ++i) {
+                    const uint32_t sym = lsym[base + i];
+                    pos += sym >> 16;
+                    if (pos < 64u) row[zz[pos]] = (int16_t)(sym & 0xFFFFu);
+                    pos += 1u;
+                }
+            } else {
+                const bool pair = !__builtin_amdgcn_ballot_w64(lane >= h && lane < he && cnt_lane > 32u);
+                uint32_t sy[kGroup], cnt[kGroup];
+                if (pair)
+                    decode_loads_pair(symbols, offv, oend, h, he, lane, sy, cnt);
+                else
+                    decode_loads(symbols, offv, oend, h, nb, lane, sy, cnt);
+                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the previous half's stores, before any LDS read
+#pragma unroll
+                for (int k = 0; k < 4; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
+                if (pair) {
+                    const int half = lane >> 5, s = lane & 31;
+                    for (int g = h; g < he; g += 2 * kGroup) {
+                        uint32_t nsy[kGroup], ncnt[kGroup];
+                        decode_loads_pair(symbols, offv, oend, g + 2 * kGroup < he ? g + 2 * kGroup : g, he, lane,
+                                          nsy, ncnt);
+#pragma unroll
+                        for (int u = 0; u < kGroup; ++u) {
+                            const bool live = (uint32_t)s < cnt[u];
+                            uint32_t e = wave_inclusive_scan(live ? (sy[u] >> 16) + 1u : 0u);
+                            const uint32_t lo = __builtin_amdgcn_readlane(e, 31);  // block A's total
+                            if (half) e -= lo;
+                            const uint32_t pos = e - 1u;
+                            const int b = g + 2 * u + half;
+                            if (live && pos < 64u && b < he)
+                                *reinterpret_cast<int16_t *>(lt + (b - h) * 128 + 2 * zz[pos]) =
+                                    (int16_t)(sy[u] & 0xFFFFu);
+                        }
+#pragma unroll
+                        for (int u = 0; u < kGroup; ++u) {
+                            sy[u] = nsy[u];
+                            cnt[u] = ncnt[u];
+                        }
                     }
+                } else
+                    for (int g = h; g < he; g += kGroup) {
+                        uint32_t nsy[kGroup], ncnt[kGroup];
+                        decode_loads(symbols, offv, oend, g + kGroup < he ? g + kGroup : g, nb, lane, nsy, ncnt);
 #pragma unroll
-                    for (int u = 0; u < kGroup; ++u) {
-                        sy[u] = nsy[u];
-                        cnt[u] = ncnt[u];
+                        for (int u = 0; u < kGroup; ++u) {
+                            const uint32_t e =
+                                wave_inclusive_scan((uint32_t)lane < cnt[u] ? (sy[u] >> 16) + 1u : 0u);
+                            const uint32_t pos = e - 1u;
+                            if ((uint32_t)lane < cnt[u] && pos < 64u && g + u < he)
+                                *reinterpret_cast<int16_t *>(lt + (g - h + u) * 128 + 2 * zz[pos]) =
+                                    (int16_t)(sy[u] & 0xFFFFu);
+                        }
+#pragma unroll
+                        for (int u = 0; u < kGroup; ++u) {
+                            sy[u] = nsy[u];
+                            cnt[u] = ncnt[u];
+                        }
                     }
-                }
-            } else
-            for (int g = h; g < he; g += kGroup) {
-                uint32_t nsy[kGroup], ncnt[kGroup];
-                decode_loads(symbols, offv, oend, g + kGroup < he ? g + kGroup : g, nb, lane, nsy, ncnt);
-#pragma unroll
-                for (int u = 0; u < kGroup; ++u) {
-                    const uint32_t e = wave_inclusive_scan((uint32_t)lane < cnt[u] ? (sy[u] >> 16) + 1u : 0u);
-                    const uint32_t pos = e - 1u;
-                    if ((uint32_t)lane < cnt[u] && pos < 64u && g + u < he)
-                        *reinterpret_cast<int16_t *>(lt + (g - h + u) * 128 + 2 * zz[pos]) = (int16_t)(sy[u] & 0xFFFFu);
-                }
-#pragma unroll
-                for (int u = 0; u < kGroup; ++u) {
-                    sy[u] = nsy[u];
-                    cnt[u] = ncnt[u];
-                }
             }
             wave_sync_lds();
             u4r val[4];
