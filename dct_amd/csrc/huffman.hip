@@ -34,7 +34,8 @@
 // at most 16 / 32 nonzero coefficients (natural content), just those, compacted
 // through LDS -- adds one count per run length into its column of an LDS
 // histogram (16-bit counters, two lanes per dword, ds_add_u32), then runs the
-// bucket merge.  VALU-bound (~2000 instructions per 64 dense blocks).
+// bucket merge.  VALU-bound (~2000 instructions per 64 dense blocks; DESIGN.md 3.8).
+// DCTQ_HUF_MIN_WAVES (launch bound, default 1: 136 VGPRs, 3 waves/SIMD) is an A/B knob.
 #include "dctq_internal.h"
 
 namespace dctq {
@@ -81,18 +82,18 @@ __device__ __forceinline__ uint32_t key_of(const uint32_t (&d)[32], int i) {
 }
 
 // Runs of equal values in the sorted registers -> one histogram count per
-// distinct value at its frequency; `count` += symbols, `nodes` += distinct values.
+// distinct value at its frequency; `nodes` += distinct values.
 template <int N>
-__device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine, int lane, uint32_t &count,
-                                             uint32_t &nodes) {
+__device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine, int lane, uint32_t &nodes) {
+    // branch-free: every element adds (end ? 1 : 0) at its run length, so no
+    // per-element exec mask is live (64 of them spilled to SGPR lanes)
     uint32_t run = 1;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const bool real = a[i] != kSent;
-        const bool end = real && (i == N - 1 || a[i + 1 < N ? i + 1 : N - 1] != a[i]);
-        if (end) hist_add(mine, run, lane, 1);
-        count += real ? 1u : 0u;
-        nodes += end ? 1u : 0u;
+        const uint32_t nxt = i + 1 < N ? a[i + 1 < N ? i + 1 : N - 1] : kSent;
+        const uint32_t end = a[i] != kSent && nxt != a[i] ? 1u : 0u;
+        hist_add(mine, run, lane, end);
+        nodes += end;
         run = end ? 1u : run + 1u;
     }
 }
@@ -117,19 +118,19 @@ __device__ __forceinline__ void tile_row(const char *mine, int lane, uint32_t (&
 // the path choice and each path gets its own register allocation (a shared
 // 32-register row made the compiler hold 188-336 VGPRs).
 template <int N>
-__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &count, uint32_t &nodes) {
+__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &nodes) {
     uint32_t d[32];
     tile_row(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
     __builtin_amdgcn_wave_barrier();
+    // branch-free compaction: every key is written at the next slot, which advances
+    // only past a nonzero (a zero's write is overwritten or lies past `pos`)
     uint32_t pos = 0;
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
         const uint32_t v = key_of(d, i);
-        if (v != kSent) {
-            *reinterpret_cast<uint32_t *>(mine + (pos * 64 + lane) * 4) = v;
-            ++pos;
-        }
+        *reinterpret_cast<uint32_t *>(mine + (pos * 64 + lane) * 4) = v;
+        pos += v != kSent ? 1u : 0u;
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t b[N];
@@ -144,10 +145,10 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &coun
 #pragma unroll
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    runs_to_hist<N>(b, mine, lane, count, nodes);
+    runs_to_hist<N>(b, mine, lane, nodes);
 }
 
-__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &count, uint32_t &nodes) {
+__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes) {
     uint32_t a[64];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -165,10 +166,13 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &count
 #pragma unroll
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    runs_to_hist<64>(a, mine, lane, count, nodes);
+    runs_to_hist<64>(a, mine, lane, nodes);
 }
 
-__global__ __launch_bounds__(kHufThreads) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
+#ifndef DCTQ_HUF_MIN_WAVES
+#define DCTQ_HUF_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                    uint32_t *__restrict__ bits, long long ntiles) {
     __shared__ uint4 lds[kHufWaves * 64 * kHufPitch / 16];  // per wave: tile stage, then the histogram (8 KiB)
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -207,23 +211,35 @@ __global__ __launch_bounds__(kHufThreads) void huffman_bits_kernel(const int16_t
         // (and holding) these 32 registers across the choice
         asm volatile("" ::: "memory");
         // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
-        uint32_t count = last_zero ? 1u : 0u, nodes = count;
+        const uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
+        uint32_t nodes = last_zero ? 1u : 0u;
         if (!__builtin_amdgcn_ballot_w64(nz > 16))
-            sparse_runs<16>(mine, lane, count, nodes);
+            sparse_runs<16>(mine, lane, nodes);
         else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-            sparse_runs<32>(mine, lane, count, nodes);
+            sparse_runs<32>(mine, lane, nodes);
         else
-            dense_runs(mine, lane, count, nodes);
+            dense_runs(mine, lane, nodes);
         if (last_zero) hist_add(mine, 1, lane, 1);
-        // ---- bucket merge (see the header): wpl = sum of internal node weights
+        // ---- bucket merge (see the header): wpl = sum of internal node weights.
+        // Bucket w+1 is read at the top of iteration w, so its LDS latency hides
+        // behind the iteration; the only merges of iteration w that land on w+1
+        // (pending 1 + w, and the pairs of w = 1) are carried in a register, and
+        // every other new weight is above w+1 and was never read early.
         uint32_t wpl = 0, pending = 0;
         if (lane >= nb) nodes = 1;  // past the tail: nothing to do
+        const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [(w-1)*64]
+        uint32_t cur = bucket[0];
         for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
-            uint32_t c = *reinterpret_cast<const uint16_t *>(mine + (w - 1) * 128 + lane * 2);
+            const uint32_t nxt = w < 64 ? bucket[w * 64] : 0u;
+            uint32_t c = cur, carry = 0;
             if (nodes > 1) {
                 if (pending && c) {
-                    wpl += pending + w;
-                    hist_add(mine, pending + w, lane, 1);
+                    const uint32_t nw = pending + w;
+                    wpl += nw;
+                    if (nw == w + 1)
+                        carry = 1;
+                    else
+                        hist_add(mine, nw, lane, 1);
                     --c;
                     --nodes;
                     pending = 0;
@@ -232,10 +248,14 @@ __global__ __launch_bounds__(kHufThreads) void huffman_bits_kernel(const int16_t
                 if (pairs) {
                     wpl += pairs * 2 * w;
                     nodes -= pairs;
-                    hist_add(mine, 2 * w, lane, pairs);
+                    if (w == 1)
+                        carry += pairs;
+                    else
+                        hist_add(mine, 2 * w, lane, pairs);
                 }
                 if (c & 1) pending = w;
             }
+            cur = nxt + carry;
         }
         const __amdgpu_buffer_rsrc_t rb =
             __builtin_amdgcn_make_buffer_rsrc(bits + t * 64, (short)0, nb * 4, 0x00020000);
