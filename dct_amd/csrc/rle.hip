@@ -343,8 +343,10 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
 }
 
 // ---- decode: one wave per 64-block tile, rebuilt 32 blocks at a time in a
-// natural-order LDS copy (4 KiB per wave: 8 waves/SIMD) and written as 1 KiB
-// stores (8 lane-addresses per block).  Per block: its symbols (lane s = symbol
+// natural-order LDS copy (8 waves/SIMD) and written as 1 KiB stores (8
+// lane-addresses per block).  Each half takes one of three paths by its symbol
+// count: lane (<= 240), walk (<= DCTQ_DEC_WALK_MAX), or scan-and-scatter, which
+// follows.  Scan path, per block: its symbols (lane s = symbol
 // s, one load; the next group's loads are issued before this group is
 // scattered), an inclusive scan of run+1 gives each symbol's zigzag position
 // (run_length_decode: pos += run; zigzag[pos++] = value, dropped past the end,
@@ -353,6 +355,9 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
 // tile's LDS work starts after a vmcnt(0) that retires the previous half's
 // stores (store-data hazard); no store is issued inside the half.
 constexpr int kHalf = 32;
+#ifndef DCTQ_DEC_WALK_MAX
+#define DCTQ_DEC_WALK_MAX 1024
+#endif
 
 // offv: lane b holds offsets[64t + b] (b < nb); oend = offsets[64t + nb], the end
 // of the tile's symbols (lane 64 does not exist, and readlane(64) would wrap).
@@ -389,20 +394,34 @@ __device__ __forceinline__ void decode_loads_pair(const uint32_t *symbols, uint3
     }
 }
 
-// Lane path (a half tile of at most kDecLaneMax symbols: natural content):
-// the half's symbols come in as coalesced dword loads and go to LDS behind the
-// zeroed half tile, and lane i < 32 walks block h+i's symbols
-// (pos += run; tile[i][zigzag[pos]] = value while pos < 64; pos++) -- about 6
-// instructions per symbol per lane instead of a scan and scatter per block.
-// 4 KiB + 960 B per wave keeps 8 waves/SIMD (the dense path needs them).
+// Walk path (a half tile of at most kDecWalkMax symbols): lane i < 32 rebuilds
+// block h+i on its own -- its symbols as 16-B loads (four per lane-address,
+// the next kDecBatch in flight while these are placed), each value written at
+// zigzag[pos] of its row in a zeroed natural-order half tile (pos += run; put
+// while pos < 64; pos++).  The row pitch is 144 B: a symbol past position 63
+// or past the block's count lands in the row's 16-B padding, so placement is
+// branch-free.  A block's count is clamped to 64, which bounds the walk for
+// any offsets.  Denser halves take the scan-and-scatter path (pitch 128).
+// 4.5 KiB per wave keeps 8 waves/SIMD.
+//
+// Lane path (a half tile of at most kDecLaneMax symbols: natural content): the
+// half's symbols come in as coalesced dword loads and go to LDS behind the
+// zeroed half tile (pitch 128), and lane i < 32 walks block h+i's symbols from
+// there, clamped to the half's symbols.  Faster than the walk path at this
+// density (one coalesced load per 64 symbols instead of per-lane 16-B loads).
+//
+// 4 KiB + 960 B per wave keeps 8 waves/SIMD (the scan path needs them).
 #ifdef DCTQ_RLE_WAVE_ONLY
-constexpr uint32_t kDecLaneMax = 0;
+constexpr uint32_t kDecLaneMax = 0, kDecWalkMax = 0;
 #else
-constexpr uint32_t kDecLaneMax = 240;
+constexpr uint32_t kDecLaneMax = 240, kDecWalkMax = DCTQ_DEC_WALK_MAX;
 #endif
-constexpr int kDecLds = kHalf * 128 + 240 * 4;
+constexpr int kDecPitch = 144;
+constexpr int kDecBatch = 16;  // symbols per lane per step
+constexpr int kDecLds = kHalf * 128 + 240 * 4;  // >= kHalf * kDecPitch
+static_assert(kDecLds >= kHalf * kDecPitch, "walk path tile");
 
-__global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t *__restrict__ symbols,
+__global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32_t *__restrict__ symbols,
                                                                  const uint32_t *__restrict__ offsets, long long nblk,
                                                                  int16_t *__restrict__ coef, long long ntiles) {
     __shared__ u4r wave_lds[kRleWaves][kDecLds / 16];
@@ -424,7 +443,9 @@ __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t 
         for (int h = 0; h < nb; h += kHalf) {
             const int he = nb < h + kHalf ? nb : h + kHalf;
             const uint32_t s0 = __builtin_amdgcn_readlane(offv, h), nh = off_at(offv, oend, he) - s0;
-            if (kDecLaneMax && nh <= kDecLaneMax) {
+            const bool lane_path = kDecLaneMax && nh <= kDecLaneMax;
+            const bool walk = !lane_path && kDecWalkMax && nh <= kDecWalkMax;
+            if (lane_path) {
                 const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
                 uint32_t v[4];
@@ -453,6 +474,47 @@ __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t 
                     pos += sym >> 16;
                     if (pos < 64u) row[zz[pos]] = (int16_t)(sym & 0xFFFFu);
                     pos += 1u;
+                }
+            } else if (walk) {
+                // the half's symbols; loads past them (any lane, any offsets) are clipped to 0
+                const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
+                const uint32_t my_off = (uint32_t)__shfl((int)offv, (lane + h) & 63);
+                const uint32_t my_cnt = (uint32_t)__shfl((int)cnt_lane, (lane + h) & 63);
+                const uint32_t cnt = lane < he - h ? (my_cnt < 64u ? my_cnt : 64u) : 0u;
+                const uint32_t rel = (my_off - s0) * 4u;
+                auto load_batch = [&](uint32_t i, u4r (&q)[kDecBatch / 4]) {
+#pragma unroll
+                    for (int k = 0; k < kDecBatch / 4; ++k)
+                        q[k] = i + 4 * k < cnt
+                                   ? __builtin_amdgcn_raw_buffer_load_b128(rsy, rel + (i + 4 * k) * 4u, 0, 0)
+                                   : u4r{0u, 0u, 0u, 0u};
+                };
+                u4r cur[kDecBatch / 4];
+                load_batch(0, cur);
+                // vmcnt(0) before any LDS read into registers: the previous half's stores
+                // (store-data hazard); the walk's own loads are in the same count
+                __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    if (k < 4 || lane < 32) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
+                wave_sync_lds();
+                char *row = lt + (lane & 31) * kDecPitch;
+                uint32_t pos = 0;
+                for (uint32_t i = 0; __builtin_amdgcn_ballot_w64(i < cnt); i += kDecBatch) {
+                    u4r nxt[kDecBatch / 4];
+                    load_batch(i + kDecBatch, nxt);
+#pragma unroll
+                    for (int j = 0; j < kDecBatch; ++j) {
+                        const uint32_t sym = cur[j >> 2][j & 3];
+                        pos += sym >> 16;
+                        const bool put = pos < 64u && i + j < cnt;
+                        const uint32_t at = put ? 2u * zz[pos < 64u ? pos : 63u] : 128u;  // 128: the padding
+                        *reinterpret_cast<int16_t *>(row + at) = (int16_t)(sym & 0xFFFFu);
+                        pos += 1u;
+                    }
+#pragma unroll
+                    for (int k = 0; k < kDecBatch / 4; ++k) cur[k] = nxt[k];
                 }
             } else {
                 const bool pair = !__builtin_amdgcn_ballot_w64(lane >= h && lane < he && cnt_lane > 32u);
@@ -509,9 +571,12 @@ __global__ __launch_bounds__(kRleThreads) void rle_decode_kernel(const uint32_t 
                     }
             }
             wave_sync_lds();
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the walk's last (clipped) loads before the read-out
             u4r val[4];
+            const int pitch = walk ? kDecPitch : 128;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) val[k] = reinterpret_cast<const u4r *>(lt)[k * 64 + lane];
+            for (int k = 0; k < 4; ++k)
+                val[k] = *reinterpret_cast<const u4r *>(lt + (8 * k + (lane >> 3)) * pitch + 16 * (lane & 7));
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(coef + (b0 + h) * 64, (short)0, (he - h) * 128, 0x00020000);
 #pragma unroll

@@ -627,9 +627,11 @@ def test_rle_bit_exact_and_round_trip(T, dm):
         return b
     # emit's two paths (rle.hip): tiles of <= 1024 symbols go lane-per-block through LDS, denser
     # ones wave-per-block -- tiles at 1024 / 1025 symbols, alternating tiles, a ragged sparse tail;
-    # decode's: half tiles (32 blocks) of <= 240 symbols lane-per-block -- halves at 240 / 241
+    # decode's: half tiles (32 blocks) of <= 240 symbols lane path, <= 1024 walk path, denser scan path --
+    # halves at 240 / 241 and 1024 / 1025 symbols, and walk halves with 64-symbol blocks
     cases.append(blocks_with([16] * 64 + [16] * 63 + [17] + [1] * 64 + [64] * 64 + [2] * 64 + [40] * 64
-                             + [7] * 16 + [8] * 16 + [7] * 15 + [8] * 17 + [3] * 29))
+                             + [7] * 16 + [8] * 16 + [7] * 15 + [8] * 17 + [32] * 32 + [32] * 31 + [33]
+                             + [64] * 8 + [1] * 24 + [3] * 29))
     for c in cases:
         off, sym = dm.rle_encode(T.from_numpy(c).cuda())
         woff, wsym = O.rle_encode_plane(c)
