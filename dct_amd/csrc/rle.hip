@@ -212,9 +212,13 @@ constexpr int kEmitLds = 64 * kEmitPitch;
 #ifdef DCTQ_RLE_WAVE_ONLY  // A/B switch (tools/rle_ab.py): every emit/decode tile takes the wave-per-block path
 constexpr uint32_t kLaneWalkMax = 0;
 #else
-constexpr uint32_t kLaneWalkMax = 1024;  // symbols of a tile the lane-per-block path stages (<= kEmitLds / 4)
+#ifndef DCTQ_EMIT_WALK_MAX
+#define DCTQ_EMIT_WALK_MAX 2048
 #endif
-constexpr int kMaxChunks = 16;  // kLaneWalkMax / 64
+constexpr uint32_t kLaneWalkMax = DCTQ_EMIT_WALK_MAX;  // symbols of a tile the lane-per-block path stages
+static_assert(kLaneWalkMax <= kEmitLds / 4 && kLaneWalkMax <= 2048, "two flush rounds of 1 024");
+#endif
+constexpr int kMaxChunks = 16;  // chunks of 64 symbols per flush round
 
 // A tile whose symbols fit the wave's LDS (natural content: ~6 symbols per
 // block) is walked lane-per-block: lane b reads block b's row, walks its 64
@@ -299,18 +303,26 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
             const uint32_t nrec = (uint32_t)(room < nsym ? room : nsym) * 4u;
             const __amdgpu_buffer_rsrc_t rsym =
                 __builtin_amdgcn_make_buffer_rsrc(symbols + o0, (short)0, (int)nrec, 0x00020000);
-            // all LDS reads first, then the stores (store-data hazard); chunks
-            // of 64 symbols in guarded groups of 4, the tail clipped by num_records
-            uint32_t v[kMaxChunks];
+            // all LDS reads of a round first, then its stores (store-data hazard):
+            // chunks of 64 symbols in guarded groups of 4, the tail clipped by num_records;
+            // a second round (past 1 024 symbols) starts after a vmcnt(0)
 #pragma unroll
-            for (int j = 0; j < kMaxChunks; ++j) v[j] = *reinterpret_cast<const uint32_t *>(lt + (j * 64 + lane) * 4);
+            for (int r = 0; r < (int)((kLaneWalkMax + 1023) / 1024); ++r) {
+                if (r * 1024 >= (int)nsym) break;
+                if (r) __builtin_amdgcn_s_waitcnt(0x0F70);
+                uint32_t v[kMaxChunks];
 #pragma unroll
-            for (int g = 0; g < kMaxChunks; g += 4)
-                if (g * 64 < (int)nsym) {
+                for (int j = 0; j < kMaxChunks; ++j)
+                    v[j] = *reinterpret_cast<const uint32_t *>(lt + ((r * kMaxChunks + j) * 64 + lane) * 4);
 #pragma unroll
-                    for (int j = g; j < g + 4; ++j)
-                        __builtin_amdgcn_raw_buffer_store_b32(v[j], rsym, (j * 64 + lane) * 4, 0, 0);
-                }
+                for (int g = 0; g < kMaxChunks; g += 4)
+                    if ((r * kMaxChunks + g) * 64 < (int)nsym) {
+#pragma unroll
+                        for (int j = g; j < g + 4; ++j)
+                            __builtin_amdgcn_raw_buffer_store_b32(v[j], rsym, ((r * kMaxChunks + j) * 64 + lane) * 4,
+                                                                  0, 0);
+                    }
+            }
             continue;
         }
         uint32_t z[32];  // two blocks' elements per register (64 live VGPRs would halve the occupancy)

@@ -625,13 +625,14 @@ def test_rle_bit_exact_and_round_trip(T, dm):
         for i, k in enumerate(counts):
             b[i, rng.permutation(63)[:k - 1]] = rng.integers(1, 300, k - 1) * rng.choice([-1, 1], k - 1)
         return b
-    # emit's two paths (rle.hip): tiles of <= 1024 symbols go lane-per-block through LDS, denser
-    # ones wave-per-block -- tiles at 1024 / 1025 symbols, alternating tiles, a ragged sparse tail;
+    # emit's two paths (rle.hip): tiles of <= 2048 symbols go lane-per-block through LDS (flushed in
+    # rounds of 1024), denser ones wave-per-block -- tiles at 1024 / 1025 and 2048 / 2049 symbols,
+    # alternating tiles, a ragged sparse tail;
     # decode's: half tiles (32 blocks) of <= 240 symbols lane path, <= 1024 walk path, denser scan path --
     # halves at 240 / 241 and 1024 / 1025 symbols, and walk halves with 64-symbol blocks
     cases.append(blocks_with([16] * 64 + [16] * 63 + [17] + [1] * 64 + [64] * 64 + [2] * 64 + [40] * 64
                              + [7] * 16 + [8] * 16 + [7] * 15 + [8] * 17 + [32] * 32 + [32] * 31 + [33]
-                             + [64] * 8 + [1] * 24 + [3] * 29))
+                             + [64] * 8 + [1] * 24 + [32] * 64 + [32] * 63 + [33] + [3] * 29))
     for c in cases:
         off, sym = dm.rle_encode(T.from_numpy(c).cuda())
         woff, wsym = O.rle_encode_plane(c)
