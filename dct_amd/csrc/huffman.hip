@@ -34,7 +34,8 @@
 // at most 16 / 32 nonzero coefficients (natural content), just those, compacted
 // through LDS -- adds one count per run length into its column of an LDS
 // histogram (16-bit counters, two lanes per dword, ds_add_u32), then runs the
-// bucket merge.  VALU-bound (~2000 instructions per 64 dense blocks).
+// bucket merge.  Dense tiles whose every block's values span < 64 integers
+// (q50 noise, most natural content) skip the sort: dense_counts below.  VALU-bound (~2000 instructions per 64 dense blocks).
 // DCTQ_HUF_MIN_WAVES (launch bound, default 1: 136 VGPRs, 3 waves/SIMD) is an A/B knob.
 #include "dctq_internal.h"
 
@@ -43,6 +44,7 @@ namespace dctq {
 constexpr int kHufWaves = 4;
 constexpr int kHufThreads = 64 * kHufWaves;
 constexpr int kHufPitch = 144;  // bytes per block in the tile stage (128 + 16: ds_read_b128 spread)
+constexpr int kHufWaveLds = 12288;  // >= 64 * kHufPitch and 8 KiB histogram + 4 KiB counters
 
 __device__ __forceinline__ void cas(uint32_t &a, uint32_t &b) {
     const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
@@ -169,14 +171,56 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
     runs_to_hist<64>(a, mine, lane, nodes);
 }
 
+// Dense tiles whose every block's nonzero values span fewer than 64 integers
+// (q50 natural or noise content): no sort.  Lane b counts its values in 64
+// 8-bit counters (value - min) in its LDS column past the histogram (16 dwords,
+// dword k*64 + lane: conflict-free, ds_add_u32), then each nonzero counter is
+// one distinct value of that frequency.  ~850 VALU per 64 blocks against ~1 470
+// for the 64-network and its run scan.
+constexpr int kHufCnt = 8192;  // byte offset of the counters in the wave's LDS (after the histogram)
+
+__device__ __forceinline__ int32_t coef_at(const uint32_t (&d)[32], int i) {
+    return (i & 1) ? (int32_t)d[i >> 1] >> 16 : (int32_t)(int16_t)(d[i >> 1] & 0xFFFFu);
+}
+
+__device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin, uint32_t &nodes) {
+    uint32_t d[32];
+    tile_row(mine, lane, d);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the row is in registers before the tile is overwritten
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 12; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+    char *cnt = mine + kHufCnt + lane * 4;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        const int32_t v = coef_at(d, i);
+        const uint32_t s = (uint32_t)(v - vmin) & 63u;
+        __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(cnt + (s >> 2) * 256), (v != 0 ? 1u : 0u) << (8 * (s & 3)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t w = *reinterpret_cast<const uint32_t *>(cnt + k * 256);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t f = (w >> (8 * b)) & 0xFFu;
+            hist_add(mine, f ? f : 1u, lane, f ? 1u : 0u);  // branch-free (an add of 0 for an empty counter)
+            nodes += f ? 1u : 0u;
+        }
+    }
+}
+
 #ifndef DCTQ_HUF_MIN_WAVES
 #define DCTQ_HUF_MIN_WAVES 1
 #endif
 __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                    uint32_t *__restrict__ bits, long long ntiles) {
-    __shared__ uint4 lds[kHufWaves * 64 * kHufPitch / 16];  // per wave: tile stage, then the histogram (8 KiB)
+    // per wave: the tile stage (9 KiB), then the histogram (8 KiB) and the dense counters (4 KiB)
+    __shared__ uint4 lds[kHufWaves * kHufWaveLds / 16];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    char *mine = reinterpret_cast<char *>(lds) + wv * 64 * kHufPitch;
+    char *mine = reinterpret_cast<char *>(lds) + wv * kHufWaveLds;
     const long long stride = (long long)gridDim.x * kHufWaves;
     for (long long t = (long long)blockIdx.x * kHufWaves + wv; t < ntiles; t += stride) {
         const long long left = nblk - t * 64;
@@ -200,12 +244,28 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
         __builtin_amdgcn_wave_barrier();
         uint32_t nz = 0;
         bool last_zero;  // c[63] == 0: value 0 is a symbol once
+        bool narrow = false;  // dense tile whose every block's values span < 64 integers
+        int32_t vmin = 0;
         {
             uint32_t d[32];
             tile_row(mine, lane, d);
 #pragma unroll
             for (int k = 0; k < 32; ++k) nz += ((d[k] & 0xFFFFu) != 0u) + ((d[k] >> 16) != 0u);
             last_zero = (d[31] >> 16) == 0u;
+            if (__builtin_amdgcn_ballot_w64(nz > 32)) {
+                // dense tile: the span of its values, zeros included (packed 16-bit min/max)
+                typedef short s2 __attribute__((ext_vector_type(2)));
+                s2 mn = __builtin_bit_cast(s2, d[0]), mx = mn;
+#pragma unroll
+                for (int k = 1; k < 32; ++k) {
+                    const s2 x = __builtin_bit_cast(s2, d[k]);
+                    mn = __builtin_elementwise_min(mn, x);
+                    mx = __builtin_elementwise_max(mx, x);
+                }
+                vmin = mn.x < mn.y ? mn.x : mn.y;
+                const int32_t vmax = mx.x > mx.y ? mx.x : mx.y;
+                narrow = !__builtin_amdgcn_ballot_w64(lane < nb && vmax - vmin >= 64);
+            }
         }
         // the paths re-read the row: a memory clobber keeps the compiler from reusing
         // (and holding) these 32 registers across the choice
@@ -217,6 +277,8 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
             sparse_runs<16>(mine, lane, nodes);
         else if (!__builtin_amdgcn_ballot_w64(nz > 32))
             sparse_runs<32>(mine, lane, nodes);
+        else if (narrow)
+            dense_counts(mine, lane, vmin, nodes);
         else
             dense_runs(mine, lane, nodes);
         if (last_zero) hist_add(mine, 1, lane, 1);

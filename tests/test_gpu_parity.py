@@ -686,6 +686,20 @@ def test_huffman_bits_golden_and_planes(T, dm):
             k = int(rng.integers(lo, hi + 1))
             blk[r, rng.choice(64, k, replace=False)] = rng.choice([-3, -1, 1, 2, 5, 300], k)
         cases.append(blk)
+    # the counting path of dense tiles (every block's values, zeros included, span < 64 integers): a span
+    # of exactly 63, a window clear of zero (no zeros), one value 64 times; the same tile with one block
+    # spanning 64 takes the sort path
+    blk = np.zeros((64, 64), np.int16)
+    for r in range(64):
+        k = int(rng.integers(33, 65))
+        blk[r, rng.choice(64, k, replace=False)] = rng.integers(-31, 33, k)
+    blk[0] = np.arange(-31, 33)
+    blk[1] = -100 + np.arange(64)
+    blk[2] = 5
+    cases.append(blk)
+    wide = blk.copy()
+    wide[3, 7] = 64
+    cases.append(wide)
     for kind, q, ad in [("uniform", 50, 0), ("smooth", 90, 1), ("const", 10, 0), ("extreme", 100, 0),
                         ("uniform", 1, 1)]:
         cases.append(O.forward_plane(O.synth_plane(7, O.KINDS[kind], 8 * 61, 8 * 9), q, ad))  # 549 blocks
