@@ -36,7 +36,7 @@
 // histogram (16-bit counters, two lanes per dword, ds_add_u32), then runs the
 // bucket merge.  Dense tiles whose every block's values span < 64 integers
 // (q50 noise, most natural content) skip the sort: dense_counts below.  VALU-bound (~2000 instructions per 64 dense blocks).
-// DCTQ_HUF_MIN_WAVES (launch bound, default 1: 136 VGPRs, 3 waves/SIMD) is an A/B knob.
+// DCTQ_HUF_MIN_WAVES (launch bound, default 3 waves/SIMD: 168 VGPRs) is an A/B knob.
 #include "dctq_internal.h"
 
 namespace dctq {
@@ -75,6 +75,12 @@ __device__ __forceinline__ void hist_add(char *h, int w, int lane, uint32_t n) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// Occupancy of the lane's histogram: bit w-1 set while bucket w may hold nodes
+// (the merge jumps from one occupied bucket to the next).
+__device__ __forceinline__ void mark(uint64_t &occ, uint32_t w, uint32_t n) {
+    occ |= n ? 1ull << (w - 1) : 0ull;
+}
+
 constexpr uint32_t kSent = 0xFFFFFFFFu;  // a zero coefficient (dropped)
 
 // Sort key of coefficient i of a block held as 32 dwords (two int16 each):
@@ -85,8 +91,9 @@ __device__ __forceinline__ uint32_t key_of(const uint32_t (&d)[32], int i) {
 
 // Runs of equal values in the sorted registers -> one histogram count per
 // distinct value at its frequency; `nodes` += distinct values.
-template <int N>
-__device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine, int lane, uint32_t &nodes) {
+template <int N, bool kMark>
+__device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine, int lane, uint32_t &nodes,
+                                             uint64_t &occ) {
     // branch-free: every element adds (end ? 1 : 0) at its run length, so no
     // per-element exec mask is live (64 of them spilled to SGPR lanes)
     uint32_t run = 1;
@@ -95,6 +102,7 @@ __device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine,
         const uint32_t nxt = i + 1 < N ? a[i + 1 < N ? i + 1 : N - 1] : kSent;
         const uint32_t end = a[i] != kSent && nxt != a[i] ? 1u : 0u;
         hist_add(mine, run, lane, end);
+        if (kMark) mark(occ, run, end);
         nodes += end;
         run = end ? 1u : run + 1u;
     }
@@ -120,7 +128,7 @@ __device__ __forceinline__ void tile_row(const char *mine, int lane, uint32_t (&
 // the path choice and each path gets its own register allocation (a shared
 // 32-register row made the compiler hold 188-336 VGPRs).
 template <int N>
-__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &nodes) {
+__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &nodes, uint64_t &occ) {
     uint32_t d[32];
     tile_row(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
@@ -147,10 +155,10 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
 #pragma unroll
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    runs_to_hist<N>(b, mine, lane, nodes);
+    runs_to_hist<N, false>(b, mine, lane, nodes, occ);
 }
 
-__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes) {
+__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes, uint64_t &occ) {
     uint32_t a[64];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -168,7 +176,7 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
 #pragma unroll
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    runs_to_hist<64>(a, mine, lane, nodes);
+    runs_to_hist<64, true>(a, mine, lane, nodes, occ);
 }
 
 // Dense tiles whose every block's nonzero values span fewer than 64 integers
@@ -183,7 +191,7 @@ __device__ __forceinline__ int32_t coef_at(const uint32_t (&d)[32], int i) {
     return (i & 1) ? (int32_t)d[i >> 1] >> 16 : (int32_t)(int16_t)(d[i >> 1] & 0xFFFFu);
 }
 
-__device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin, uint32_t &nodes) {
+__device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin, uint32_t &nodes, uint64_t &occ) {
     uint32_t d[32];
     tile_row(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the row is in registers before the tile is overwritten
@@ -207,13 +215,14 @@ __device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin,
         for (int b = 0; b < 4; ++b) {
             const uint32_t f = (w >> (8 * b)) & 0xFFu;
             hist_add(mine, f ? f : 1u, lane, f ? 1u : 0u);  // branch-free (an add of 0 for an empty counter)
+            mark(occ, f ? f : 1u, f);
             nodes += f ? 1u : 0u;
         }
     }
 }
 
 #ifndef DCTQ_HUF_MIN_WAVES
-#define DCTQ_HUF_MIN_WAVES 1
+#define DCTQ_HUF_MIN_WAVES 3
 #endif
 __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                    uint32_t *__restrict__ bits, long long ntiles) {
@@ -273,23 +282,59 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
         // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
         const uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
         uint32_t nodes = last_zero ? 1u : 0u;
+        uint64_t occ = last_zero ? 1ull : 0ull;
+#ifdef DCTQ_HUF_UNIFORM_MERGE
+        const bool lane_merge = false;
+#else
+        const bool lane_merge = __builtin_amdgcn_ballot_w64(nz > 32) != 0;  // the dense paths mark occ
+#endif
         if (!__builtin_amdgcn_ballot_w64(nz > 16))
-            sparse_runs<16>(mine, lane, nodes);
+            sparse_runs<16>(mine, lane, nodes, occ);
         else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-            sparse_runs<32>(mine, lane, nodes);
+            sparse_runs<32>(mine, lane, nodes, occ);
         else if (narrow)
-            dense_counts(mine, lane, vmin, nodes);
+            dense_counts(mine, lane, vmin, nodes, occ);
         else
-            dense_runs(mine, lane, nodes);
+            dense_runs(mine, lane, nodes, occ);
         if (last_zero) hist_add(mine, 1, lane, 1);
         // ---- bucket merge (see the header): wpl = sum of internal node weights.
-        // Bucket w+1 is read at the top of iteration w, so its LDS latency hides
-        // behind the iteration; the only merges of iteration w that land on w+1
-        // (pending 1 + w, and the pairs of w = 1) are carried in a register, and
-        // every other new weight is above w+1 and was never read early.
         uint32_t wpl = 0, pending = 0;
         if (lane >= nb) nodes = 1;  // past the tail: nothing to do
         const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [(w-1)*64]
+        if (lane_merge) {
+        // Dense tiles: each lane jumps to its own next occupied bucket (lowest bit of occ), so the
+        // loop runs as many steps as the busiest lane has occupied buckets, not up to
+        // its largest weight.  New weights (pending + w, 2w) are above w, so the
+        // scan order is the bucket order.  Every step merges at least one pair of a
+        // consistent histogram; the step cap only bounds the loop.
+        for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(nodes > 1); ++step) {
+            if (nodes > 1) {
+                const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
+                occ &= occ - 1ull;  // bucket w is emptied by this step
+                uint32_t c = w <= 64u ? bucket[(w - 1) * 64] : 0u;
+                if (pending && c) {
+                    const uint32_t nw = pending + w;
+                    wpl += nw;
+                    hist_add(mine, nw, lane, 1);
+                    mark(occ, nw, 1);
+                    --c;
+                    --nodes;
+                    pending = 0;
+                }
+                const uint32_t pairs = c >> 1;
+                if (pairs) {
+                    wpl += pairs * 2 * w;
+                    nodes -= pairs;
+                    hist_add(mine, 2 * w, lane, pairs);
+                    mark(occ, 2 * w, 1);
+                }
+                if (c & 1) pending = w;
+            }
+        }
+        } else {
+        // Sparse tiles (few weights): every weight in turn; bucket w+1 is read at the top of iteration w, so its
+        // LDS latency hides behind the iteration; the only merges of iteration w that
+        // land on w+1 (pending 1 + w, and the pairs of w = 1) are carried in a register
         uint32_t cur = bucket[0];
         for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
             const uint32_t nxt = w < 64 ? bucket[w * 64] : 0u;
@@ -318,6 +363,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
                 if (c & 1) pending = w;
             }
             cur = nxt + carry;
+        }
         }
         const __amdgpu_buffer_rsrc_t rb =
             __builtin_amdgcn_make_buffer_rsrc(bits + t * 64, (short)0, nb * 4, 0x00020000);
