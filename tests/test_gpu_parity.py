@@ -751,13 +751,16 @@ def test_encode_capacity_and_large(T, dm):
     multi-plane encode past one scan segment (5 4K frames + 1080p chroma) equals
     forward_quant_planes + rle_encode on the GPU."""
     import oracle as O
-    px = gpu_px(T, O.synth_plane(12, 0, 256, 128))
     plan = dm.Plan(50, 0)
-    _, off, sym = plan.encode_planes([px])
-    total = int(off[-1].item())
-    _, off2, sym2 = plan.encode_planes([px], capacity=total // 3)
-    assert np.array_equal(off.cpu().numpy(), off2.cpu().numpy())
-    assert sym2.numel() == total // 3 and np.array_equal(sym2.cpu().numpy(), sym[:total // 3].cpu().numpy())
+    for kind in (0, 1):  # dense tiles (wave-per-block emit) and sparse ones (lane-per-block emit)
+        px = gpu_px(T, O.synth_plane(12, kind, 256, 128))
+        _, off, sym = plan.encode_planes([px])
+        total = int(off[-1].item())
+        tile_end = int(off[64].item())
+        for cap in (total // 3, total - 1, tile_end, tile_end + 1, 1):
+            _, off2, sym2 = plan.encode_planes([px], capacity=cap)
+            assert np.array_equal(off.cpu().numpy(), off2.cpu().numpy())
+            assert sym2.numel() == cap and np.array_equal(sym2.cpu().numpy(), sym[:cap].cpu().numpy()), (kind, cap)
     luma = dm.synth(13, "uniform", 3840, 2160, 5)
     chroma = dm.synth(14, "smooth", 1920, 1080, 3)
     ecoefs, off, sym = plan.encode_planes([luma, chroma])
