@@ -22,6 +22,9 @@
 
 namespace dctq {
 
+#ifndef DCTQ_COUNT_POLICY
+#define DCTQ_COUNT_POLICY 2  // count's tile loads: non-temporal (A/B knob)
+#endif
 constexpr int kRleWaves = 4;
 constexpr int kRleThreads = 64 * kRleWaves;
 constexpr int kGroup = 8;  // decode: blocks whose symbol loads are in flight together
@@ -55,7 +58,7 @@ __global__ __launch_bounds__(kRleThreads) void rle_count_kernel(const int16_t *_
             const_cast<int16_t *>(coef) + tt * 64 * 64, (short)0, nb * 128, 0x00020000);  // past the tail: zeros
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, 2 /* nt */);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, DCTQ_COUNT_POLICY);
             q[k] = make_uint4(v[0], v[1], v[2], v[3]);
         }
     };

@@ -1,4 +1,4 @@
-"""A/B of dctq_rle_emit / dctq_rle_decode between the default libdct_amd.so and
+"""A/B of dctq_rle_count / dctq_rle_emit / dctq_rle_decode between the default libdct_amd.so and
 diagnostic builds (tools/ubench/libvar_*.so, tools/ubench/variant.sh), same inputs,
 interleaved, HIP events; outputs must match the default build.
 
@@ -24,6 +24,7 @@ for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libvar_*.so")))
     L = C.CDLL(p)
     L.dctq_rle_emit.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p]
     L.dctq_rle_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p]
+    L.dctq_rle_count.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p]
     libs[os.path.basename(p)[7:-3]] = L
 s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 vp = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
@@ -36,8 +37,11 @@ for kind, q in (("uniform", 50), ("smooth", 50), ("smooth", 90), ("const", 50), 
     # the variants' stores on different physical pages (seen: +-12 % on identical code)
     out_sym = torch.empty_like(sym)
     back = torch.empty_like(coef)
+    out_off = torch.empty_like(off)
+    ws = torch.empty(int(dct_amd.lib().dctq_rle_workspace_bytes(nblk)) // 4 + 1, dtype=torch.int32, device="cuda")
     jobs = {}
     for k, L in libs.items():
+        jobs[f"count {k}"] = (lambda L=L: L.dctq_rle_count(vp(coef), nblk, vp(out_off), vp(ws), s), k, "count")
         jobs[f"emit {k}"] = (lambda L=L: L.dctq_rle_emit(vp(coef), nblk, vp(off), vp(out_sym), s), k, "emit")
         jobs[f"decode {k}"] = (lambda L=L: L.dctq_rle_decode(vp(sym), vp(off), nblk, vp(back), s), k, "decode")
     times = {j: [] for j in jobs}
@@ -51,7 +55,9 @@ for kind, q in (("uniform", 50), ("smooth", 50), ("smooth", 90), ("const", 50), 
             if r:
                 times[j].append(e0.elapsed_time(e1) * 1e-3)
             if r == 0:
-                if op == "emit":
+                if op == "count":
+                    assert torch.equal(out_off, off), f"{k}: count output differs"
+                elif op == "emit":
                     assert torch.equal(out_sym, ref_sym), f"{k}: emit output differs"
                 else:
                     assert torch.equal(back, coef), f"{k}: decode output differs"
