@@ -288,6 +288,10 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
 #else
         const bool lane_merge = __builtin_amdgcn_ballot_w64(nz > 32) != 0;  // the dense paths mark occ
 #endif
+#ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
+        if (true) {
+        } else
+#endif
         if (!__builtin_amdgcn_ballot_w64(nz > 16))
             sparse_runs<16>(mine, lane, nodes, occ);
         else if (!__builtin_amdgcn_ballot_w64(nz > 32))
