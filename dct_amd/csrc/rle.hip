@@ -96,7 +96,6 @@ __global__ __launch_bounds__(kRleThreads) void rle_count_kernel(const int16_t *_
 constexpr int kScanThreads = 1024;
 constexpr int kScanPer = 8;
 constexpr int kSegTilesLog2 = 13;  // 1024 * 8 tiles per segment
-constexpr int kSegBlocksLog2 = kSegTilesLog2 + 6;
 
 __global__ __launch_bounds__(kScanThreads) void rle_scan_tiles_kernel(uint32_t *__restrict__ tiles, long long ntiles,
                                                                       uint32_t *__restrict__ segs) {
