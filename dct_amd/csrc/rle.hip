@@ -432,6 +432,10 @@ constexpr uint32_t kDecLaneMax = 240, kDecWalkMax = DCTQ_DEC_WALK_MAX;
 #endif
 constexpr int kDecPitch = 144;
 constexpr int kDecBatch = 16;  // symbols per lane per step
+#ifndef DCTQ_DEC_QUAD
+#define DCTQ_DEC_QUAD 1
+#endif
+constexpr bool kDecQuad = DCTQ_DEC_QUAD;  // halves above the walk path: the quad path instead of the scan path
 constexpr int kDecLds = kHalf * 128 + 240 * 4;  // >= kHalf * kDecPitch
 static_assert(kDecLds >= kHalf * kDecPitch, "walk path tile");
 
@@ -459,6 +463,7 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
             const uint32_t s0 = __builtin_amdgcn_readlane(offv, h), nh = off_at(offv, oend, he) - s0;
             const bool lane_path = kDecLaneMax && nh <= kDecLaneMax;
             const bool walk = !lane_path && kDecWalkMax && nh <= kDecWalkMax;
+            const bool quad = kDecQuad && !lane_path && !walk;
             if (lane_path) {
                 const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
@@ -530,6 +535,58 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
 #pragma unroll
                     for (int k = 0; k < kDecBatch / 4; ++k) cur[k] = nxt[k];
                 }
+            } else if (quad) {
+                // Quad path: 4 blocks per step, one per 16-lane row; lane s of a row holds its
+                // block's symbols 4s..4s+3 (one 16-B load: 4 symbols per lane-address). Positions:
+                // a 4-element prefix in the lane, then a row-segmented DPP scan of the lane totals.
+                const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
+                const int r = lane >> 4, s4 = 4 * (lane & 15);
+                auto group_load = [&](int g, u4r &q, uint32_t &cnt) {
+                    const int b = h + 4 * g + r;  // this row's block (past `he`: none)
+                    const uint32_t ob = (uint32_t)__shfl((int)offv, b & 63);
+                    const uint32_t cb = (uint32_t)__shfl((int)cnt_lane, b & 63);
+                    cnt = b < he ? (cb < 64u ? cb : 64u) : 0u;
+                    q = (uint32_t)s4 < cnt ? __builtin_amdgcn_raw_buffer_load_b128(rsy, (ob - s0 + s4) * 4u, 0, 0)
+                                           : u4r{0u, 0u, 0u, 0u};
+                };
+                const int ng = (he - h + 3) >> 2;
+                u4r q;
+                uint32_t cnt;
+                group_load(0, q, cnt);
+                // vmcnt(0) before any LDS read into registers: the previous half's stores (store-data hazard)
+                __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+                for (int k = 0; k < 5; ++k)
+                    if (k < 4 || lane < 32) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
+                wave_sync_lds();
+                for (int g = 0; g < ng; ++g) {
+                    u4r nq;
+                    uint32_t ncnt;
+                    group_load(g + 1 < ng ? g + 1 : g, nq, ncnt);
+                    uint32_t p[4], run = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        run += (uint32_t)s4 + j < cnt ? (q[j] >> 16) + 1u : 0u;
+                        p[j] = run;
+                    }
+                    uint32_t incl = run;  // row-segmented inclusive scan of the lane totals
+                    incl += __builtin_amdgcn_update_dpp(0u, incl, 0x111, 0xF, 0xF, false);  // row_shr:1
+                    incl += __builtin_amdgcn_update_dpp(0u, incl, 0x112, 0xF, 0xF, false);  // row_shr:2
+                    incl += __builtin_amdgcn_update_dpp(0u, incl, 0x114, 0xF, 0xF, false);  // row_shr:4
+                    incl += __builtin_amdgcn_update_dpp(0u, incl, 0x118, 0xF, 0xF, false);  // row_shr:8
+                    const uint32_t before = incl - run;
+                    char *row = lt + (4 * g + r) * kDecPitch;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t pos = before + p[j] - 1u;
+                        const bool put = (uint32_t)s4 + j < cnt && pos < 64u;
+                        const uint32_t at = put ? 2u * zz[pos < 64u ? pos : 63u] : 128u;  // 128: the padding
+                        *reinterpret_cast<int16_t *>(row + at) = (int16_t)(q[j] & 0xFFFFu);
+                    }
+                    q = nq;
+                    cnt = ncnt;
+                }
             } else {
                 const bool pair = !__builtin_amdgcn_ballot_w64(lane >= h && lane < he && cnt_lane > 32u);
                 uint32_t sy[kGroup], cnt[kGroup];
@@ -587,7 +644,7 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
             wave_sync_lds();
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the walk's last (clipped) loads before the read-out
             u4r val[4];
-            const int pitch = walk ? kDecPitch : 128;
+            const int pitch = walk || quad ? kDecPitch : 128;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 val[k] = *reinterpret_cast<const u4r *>(lt + (8 * k + (lane >> 3)) * pitch + 16 * (lane & 7));
