@@ -91,9 +91,9 @@ __device__ __forceinline__ uint32_t key_of(const uint32_t (&d)[32], int i) {
 
 // Runs of equal values in the sorted registers -> one histogram count per
 // distinct value at its frequency; `nodes` += distinct values.
-template <int N, bool kMark>
+template <int N, bool kMax>
 __device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine, int lane, uint32_t &nodes,
-                                             uint64_t &occ) {
+                                             uint32_t &lmax) {
     // branch-free: every element adds (end ? 1 : 0) at its run length, so no
     // per-element exec mask is live (64 of them spilled to SGPR lanes)
     uint32_t run = 1;
@@ -102,7 +102,7 @@ __device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine,
         const uint32_t nxt = i + 1 < N ? a[i + 1 < N ? i + 1 : N - 1] : kSent;
         const uint32_t end = a[i] != kSent && nxt != a[i] ? 1u : 0u;
         hist_add(mine, run, lane, end);
-        if (kMark) mark(occ, run, end);
+        if (kMax) lmax = end && run > lmax ? run : lmax;
         nodes += end;
         run = end ? 1u : run + 1u;
     }
@@ -128,7 +128,7 @@ __device__ __forceinline__ void tile_row(const char *mine, int lane, uint32_t (&
 // the path choice and each path gets its own register allocation (a shared
 // 32-register row made the compiler hold 188-336 VGPRs).
 template <int N>
-__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &nodes, uint64_t &occ) {
+__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &nodes, uint32_t &lmax) {
     uint32_t d[32];
     tile_row(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
@@ -155,10 +155,10 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
 #pragma unroll
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    runs_to_hist<N, false>(b, mine, lane, nodes, occ);
+    runs_to_hist<N, false>(b, mine, lane, nodes, lmax);
 }
 
-__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes, uint64_t &occ) {
+__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes, uint32_t &lmax) {
     uint32_t a[64];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -176,7 +176,7 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
 #pragma unroll
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
-    runs_to_hist<64, true>(a, mine, lane, nodes, occ);
+    runs_to_hist<64, true>(a, mine, lane, nodes, lmax);
 }
 
 // Dense tiles whose every block's nonzero values span fewer than 64 integers
@@ -191,7 +191,7 @@ __device__ __forceinline__ int32_t coef_at(const uint32_t (&d)[32], int i) {
     return (i & 1) ? (int32_t)d[i >> 1] >> 16 : (int32_t)(int16_t)(d[i >> 1] & 0xFFFFu);
 }
 
-__device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin, uint32_t &nodes, uint64_t &occ) {
+__device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin, uint32_t &nodes, uint32_t &lmax) {
     uint32_t d[32];
     tile_row(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the row is in registers before the tile is overwritten
@@ -215,7 +215,7 @@ __device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin,
         for (int b = 0; b < 4; ++b) {
             const uint32_t f = (w >> (8 * b)) & 0xFFu;
             hist_add(mine, f ? f : 1u, lane, f ? 1u : 0u);  // branch-free (an add of 0 for an empty counter)
-            mark(occ, f ? f : 1u, f);
+            lmax = f > lmax ? f : lmax;
             nodes += f ? 1u : 0u;
         }
     }
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
         // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
         const uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
         uint32_t nodes = last_zero ? 1u : 0u;
-        uint64_t occ = last_zero ? 1ull : 0ull;
+        uint32_t lmax = last_zero ? 1u : 0u;  // the largest leaf weight (dense paths)
 #ifdef DCTQ_HUF_UNIFORM_MERGE
         const bool lane_merge = false;
 #else
@@ -293,19 +293,27 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
         } else
 #endif
         if (!__builtin_amdgcn_ballot_w64(nz > 16))
-            sparse_runs<16>(mine, lane, nodes, occ);
+            sparse_runs<16>(mine, lane, nodes, lmax);
         else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-            sparse_runs<32>(mine, lane, nodes, occ);
+            sparse_runs<32>(mine, lane, nodes, lmax);
         else if (narrow)
-            dense_counts(mine, lane, vmin, nodes, occ);
+            dense_counts(mine, lane, vmin, nodes, lmax);
         else
-            dense_runs(mine, lane, nodes, occ);
+            dense_runs(mine, lane, nodes, lmax);
         if (last_zero) hist_add(mine, 1, lane, 1);
         // ---- bucket merge (see the header): wpl = sum of internal node weights.
         uint32_t wpl = 0, pending = 0;
         if (lane >= nb) nodes = 1;  // past the tail: nothing to do
         const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [(w-1)*64]
+        uint64_t occ = 0;
         if (lane_merge) {
+            // occupancy of the leaf buckets, read back up to the wave's largest leaf weight
+            // (cheaper than marking every leaf; this wave's LDS atomics are already ordered)
+#pragma unroll
+            for (uint32_t w = 1; w <= 8; ++w)  // independent reads, in flight together
+                occ |= bucket[(w - 1) * 64] ? 1ull << (w - 1) : 0ull;
+            for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w)
+                occ |= bucket[(w - 1) * 64] ? 1ull << (w - 1) : 0ull;
         // Dense tiles: each lane jumps to its own next occupied bucket (lowest bit of occ), so the
         // loop runs as many steps as the busiest lane has occupied buckets, not up to
         // its largest weight.  New weights (pending + w, 2w) are above w, so the
