@@ -44,6 +44,11 @@ for step in "$@"; do
     ceil2) run ceil2 120 tools/ubench/stream_ceiling2 ;;
     ceil3) run ceil3 120 tools/ubench/stream_ceiling3 ;;
     ceil4) run ceil4 180 tools/ubench/stream_ceiling4 ;;
+    mix) run mix 300 tools/ubench/hbm_mix 2 ;;
+    mix2) run mix2 300 tools/ubench/hbm_mix2 10 ;;
+    mix3) run mix3 300 tools/ubench/hbm_mix3 10 ;;
+    mix4) run mix4 300 tools/ubench/hbm_mix4 10 ;;
+    phase) run phase 120 tools/ubench/hbm_phase 8 ;;
     planes) run planes 300 python tools/plane_bench.py ;;
     legacy) run legacy 120 host/legacy_latency ;;
     rleab) run rleab 300 python tools/rle_ab.py ;;

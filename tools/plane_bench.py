@@ -33,6 +33,9 @@ cases = {
     "luma": (ny, lambda: plan.forward_quant(y, out=oy)),
     "chroma": (nc, lambda: plan.forward_quant(c, out=oc)),
     "luma+chroma (one launch)": (ny + nc, lambda: plan.forward_quant_planes([y, c], outs=[oy, oc])),
+    "movement luma": (ny, lambda: plan.diag_movement_planes([y], [oy])),
+    "movement chroma": (nc, lambda: plan.diag_movement_planes([c], [oc])),
+    "movement luma+chroma": (ny + nc, lambda: plan.diag_movement_planes([y, c], [oy, oc])),
 }
 for _, fn in cases.values():
     fn()
