@@ -5,7 +5,8 @@ the first build's (bit-exact builds must agree).
 
     python tools/lib_ab.py [--rounds 12] [--kind uniform] [--quality 50] [--adaptive 0] LIB...
 
-LIB = path of a .so (tools/ubench/variant.sh / policy.sh output) or "default".
+LIB = path of a .so (tools/ubench/variant.sh / policy.sh output), "default", or
+"movement" (the default build's dctq_diag_movement_planes: the same bytes, no math).
 """
 import argparse
 import ctypes as C
@@ -42,18 +43,22 @@ stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 builds = {}
 for path in args.libs:
-    p = dct_amd.LIB_PATH if path == "default" else os.path.abspath(path)
+    p = dct_amd.LIB_PATH if path in ("default", "movement") else os.path.abspath(path)
     L = C.CDLL(p)
     L.dctq_plan_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.dctq_forward_quant_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p, C.c_void_p,
                                             C.c_void_p]
     h = C.c_void_p()
     assert L.dctq_plan_create(args.quality, args.adaptive, C.byref(h)) == 0
+    L.dctq_diag_movement_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p, C.c_void_p]
     builds[os.path.basename(path)] = (L, h)
 
 
-def launch(L, h):
-    rc = L.dctq_forward_quant_planes(h, descs, len(planes), C.cast(optr, C.c_void_p), None, stream)
+def launch(L, h, name=""):
+    if name == "movement":
+        rc = L.dctq_diag_movement_planes(h, descs, len(planes), C.cast(optr, C.c_void_p), stream)
+    else:
+        rc = L.dctq_forward_quant_planes(h, descs, len(planes), C.cast(optr, C.c_void_p), None, stream)
     assert rc == 0, rc
 
 
@@ -61,7 +66,7 @@ ref = None
 for name, (L, h) in builds.items():
     for o in outs:
         o.zero_()
-    launch(L, h)
+    launch(L, h, name)
     torch.cuda.synchronize()
     got = [o.clone() for o in outs]
     if ref is None:
@@ -73,7 +78,7 @@ for r in range(args.rounds + 2):
     for name, (L, h) in builds.items():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        launch(L, h)
+        launch(L, h, name)
         e1.record()
         torch.cuda.synchronize()
         if r >= 2:
