@@ -19,14 +19,19 @@ Another ("encode") runs the encoder (forward + zigzag run-length
 symbols) over the frames, and at N>1 the all-gather of the symbol streams.  At N>1 a
 second, separately reported leg ("gather") times forward DCT+quant of the luma frames followed by the RCCL
 all-gather of every rank's int16 coefficient planes (BASELINE configs[3],
-SURVEY 8(e)(ii)): end-to-end blocks/s including the xGMI exchange; and "band"
-splits ONE 4K 4:2:0 frame across the ranks in block-row bands and all-gathers
-its coefficient planes (latency per frame).
+SURVEY 8(e)(ii)) -- strong scaling: --total-frames 4K luma frames (64) split
+over the ranks, the kernel-only aggregate rate and the rate including the
+xGMI exchange reported apart; and "band" splits ONE 4K 4:2:0 frame across the
+ranks in block-row bands and all-gathers its coefficient planes (latency per
+frame).
 
 Also reported: the dominant kernel's roofline (algorithmic 192 B/block over the
-HIP-event-timed launch durations) and the reference's own CPU path
-(oracle/_ref/libref.so: src/dct.c + src/quantization.c compiled from
-/root/reference) timed on this host's cores in the same run.  That CPU leg
+HIP-event-timed launch durations), the memory ceilings of its traffic measured
+on the same box (roofline.movement_ceiling: its own movement and the best flat
+1:2 stream; roofline.hw_ceilings), and the reference's own CPU path
+(oracle/_ref/libref.so and libref_O0.so: src/dct.c + src/quantization.c
+compiled from /root/reference with -O2 and with the Justfile's -g) timed on
+this host's cores in the same run, all cores and one thread.  That CPU leg
 (cpu_leg, rank 0) is also where the oracle checks this run's GPU outputs (one
 chroma plane's coefficients and Huffman sizes): oracle/ is a checker here,
 never the thing measured.
@@ -61,10 +66,13 @@ def parse():
     ap.add_argument("--adaptive", type=int, default=0)
     ap.add_argument("--kind", default="uniform")
     ap.add_argument("--seed", type=int, default=12345)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (wall s)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="CPU-baseline sample budget (wall s, over its four builds x thread counts)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
+    ap.add_argument("--total-frames", type=int, default=64,
+                    help="N>1 gather leg (BASELINE configs[3]): 4K luma frames in total, split over the ranks")
     ap.add_argument("--encode-steps", type=int, default=3,
                     help="timed steps of the encoder leg (forward + zigzag/RLE symbols; at N>1 plus the "
                          "symbol-stream all-gather); 0 = skip")
@@ -79,34 +87,83 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_share():
+    """CPUs this process may use: the cgroup CPU quota if one is set, else the
+    scheduler affinity mask; capped by OMP_NUM_THREADS when the environment
+    declares a smaller share (the GPU box's harness sets it to the per-GPU share
+    of the host's cores).  Returns (threads, how)."""
+    aff = len(os.sched_getaffinity(0))
+    n, how = aff, f"affinity mask ({aff} CPUs)"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(int(quota) / int(period)))
+            if q < n:
+                n, how = q, f"cgroup cpu.max quota ({quota}/{period})"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, how = int(omp), f"OMP_NUM_THREADS={omp} (this host's CPU share per GPU; affinity {aff})"
+    return n, how
+
+
 def cpu_baseline(args):
-    """The reference CPU path on this host, bounded sample of the same workload."""
+    """The reference CPU path on this host, a bounded sample of the same workload
+    (BASELINE.md "CPU-baseline plan"): the reference's own per-block pipeline over
+    4K 4:2:0 frames, pthreads over block rows with a shared read-only ctx, built
+    with -O2 and with the Justfile's flags (-g, i.e. -O0), on every CPU of this
+    process's share (cpu_share) and on one thread.  `value` = -O2 on the share."""
     import numpy as np
     import oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    cores, share = cpu_share()
     kind = "reference" if O.ref_available() else "port"
     frames = [O.synth_plane(args.seed, O.KINDS[args.kind], Y_W, Y_H),
               O.synth_plane(args.seed + 1, O.KINDS[args.kind], C_W, C_H),
               O.synth_plane(args.seed + 2, O.KINDS[args.kind], C_W, C_H)]
     outs = [np.zeros(((f.shape[0] // 8) * (f.shape[1] // 8), 64), np.int16) for f in frames]
-    nblk, t0, nfr = 0, time.perf_counter(), 0
-    while True:
-        for f, o in zip(frames, outs):
-            if kind == "reference":
-                O.ref().ref_forward_plane(f.ravel(), f.shape[1], f.shape[0], args.quality, args.adaptive,
-                                          o.ravel(), threads, 0)
-            else:
-                o[:] = O.forward_plane(f, args.quality, args.adaptive, threads)
-            nblk += o.shape[0]
-        nfr += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
-    return {"value": nblk / el, "unit": "macroblocks/s", "cores": threads, "kind": kind,
-            "sample": f"{nfr} 4K 4:2:0 frame(s) ({nblk} blocks, {args.kind}, q{args.quality}, "
-                      f"adaptive={args.adaptive}) through ref_forward_plane: create_block_from_pixels -> "
-                      f"dct_forward -> calculate_block_variance -> quantize per block, {threads} pthreads "
-                      f"over block rows, {el:.1f} s"}
+
+    def run(build, threads, budget):
+        nblk, nfr, t0 = 0, 0, time.perf_counter()
+        while True:
+            for f, o in zip(frames, outs):
+                if kind == "reference":
+                    O.ref(build).ref_forward_plane(f.ravel(), f.shape[1], f.shape[0], args.quality, args.adaptive,
+                                                   o.ravel(), threads, 0)
+                else:
+                    o[:] = O.forward_plane(f, args.quality, args.adaptive, threads)
+                nblk += o.shape[0]
+            nfr += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return {"value": nblk / el, "threads": threads, "frames": nfr, "blocks": nblk, "seconds": el}
+
+    budget = args.cpu_seconds
+    legs = {"O2_all_cores": run("O2", cores, 0.4 * budget), "O2_one_thread": run("O2", 1, 0.2 * budget)}
+    if kind == "reference":
+        legs.update({"O0_all_cores": run("O0", cores, 0.2 * budget), "O0_one_thread": run("O0", 1, 0.2 * budget)})
+    head = legs["O2_all_cores"]
+    return {"value": head["value"], "unit": "macroblocks/s", "cores": cores, "kind": kind,
+            "nproc": cores, "cpu_share": share, "machine_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"{head['frames']} 4K 4:2:0 frame(s) ({head['blocks']} blocks, {args.kind}, q{args.quality}, "
+                      f"adaptive={args.adaptive}) through the reference's create_block_from_pixels -> dct_forward -> "
+                      f"calculate_block_variance -> quantize per block (oracle/_ref/libref.so, -O2), {cores} pthreads "
+                      f"over block rows ({share}), {head['seconds']:.1f} s",
+            "builds": {k: {"blocks_per_s": v["value"], "threads": v["threads"], "blocks": v["blocks"],
+                           "seconds": round(v["seconds"], 2)} for k, v in legs.items()},
+            "flags": {"O2": "-Wall -Wextra -Werror -pedantic -std=c99 -O2 -fPIC (oracle/Makefile REFFLAGS)",
+                      "O0": "-Wall -Wextra -Werror -pedantic -std=c99 -g -fPIC (Justfile:8 CFLAGS)"}}
 
 
 def cpu_leg(args, world, fwd_check, huf_check):
@@ -178,42 +235,45 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
             "blocks_per_s": nblk * reps / el, "gathered_equals_unsharded": ok}
 
 
-def gather_leg(args, plan, luma, coef_y, world, rank, dev):
-    """Forward DCT+quant of this rank's luma frames + RCCL all-gather of all
-    ranks' coefficient planes onto every rank; max-over-ranks wall time."""
+def gather_leg(args, plan, world, rank, dev):
+    """BASELINE configs[3], strong scaling: --total-frames 4K luma frames (64)
+    split over the ranks (shard.split: 8 per GPU at N=8), forward DCT+quant of
+    each rank's frames, then the RCCL all-gather of every rank's int16
+    coefficient planes onto every rank (shard.strong_gather_leg).  Reports the
+    kernel-only aggregate (what the GPUs transform per second together) and the
+    end-to-end rate with the exchange, apart: SURVEY 8(e) prices the gather at
+    25-170x the compute, so it is bound by xGMI, not by the kernel."""
     from dct_amd import shard
-    n = coef_y.shape[0]
-    counts = [n] * world
+    lo, hi = shard.split(args.total_frames, world, rank)
+    per = (Y_W // 8) * (Y_H // 8)
+    frames = dct_amd.synth(args.seed + 200000 + lo, args.kind, Y_W, Y_H, max(hi - lo, 1), device=dev)[:hi - lo]
+    out = torch.empty(((hi - lo) * per, 64), dtype=torch.int16, device=dev)
+    counts = [(b - a) * per for a, b in (shard.split(args.total_frames, world, r) for r in range(world))]
 
-    def once():
-        plan.forward_quant(luma, out=coef_y)
-        return shard.gather_coefficients(coef_y, counts)
+    def forward(fr):
+        if fr.shape[0]:
+            plan.forward_quant(fr, out=out)
+        return out
 
-    full = once()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.gather_steps):
-        full = once()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
-    ok = bool(torch.equal(full[rank * n:(rank + 1) * n], coef_y))
+    r = shard.strong_gather_leg(forward, frames, counts, args.gather_steps, dev, torch.cuda.synchronize)
+    full, local = r["full"], r["local"]
+    off = sum(counts[:rank])
+    ok = bool(torch.equal(full[off:off + counts[rank]], local))
     be = "RCCL all_gather_into_tensor" if dist.get_backend() == "nccl" else f"{dist.get_backend()} all_gather"
-    return {"op": f"forward_quant(luma) + {be} of int16 coefficient planes",
-            "blocks_per_s": world * n * args.gather_steps / el, "ms_per_step": el / args.gather_steps * 1e3,
-            "bytes_received_per_rank": (world - 1) * n * 128, "steps": args.gather_steps,
-            "own_slice_intact": ok}
+    n = r["blocks_per_step"] * r["steps"]
+    return {"op": f"{args.total_frames} 4K luma frames split over {world} ranks: forward_quant + {be} of the int16 "
+                  "coefficient planes (BASELINE configs[3])", "scaling": "strong", "world_size": world,
+            "frames_total": args.total_frames, "frames_this_rank": hi - lo, "steps": r["steps"],
+            "kernel_blocks_per_s": n / r["kernel_s"], "kernel_ms_per_step": r["kernel_s"] / r["steps"] * 1e3,
+            "blocks_per_s": n / r["end_to_end_s"], "ms_per_step": r["end_to_end_s"] / r["steps"] * 1e3,
+            "bytes_received_per_rank": (sum(counts) - counts[rank]) * 128, "own_slice_intact": ok}
 
 
 def small_frame_leg(args, plan, dev):
     """BASELINE configs[1]: one 512x512 grayscale frame (4 096 blocks, 256 KiB in,
     512 KiB out: cache-resident, so launch-bound -- not an HBM-roofline figure),
     200 back-to-back dctq_forward_quant launches, next to the reference's CPU
-    path on the same frame (oracle/_ref, 16 threads, rank 0 only)."""
+    path on the same frame (oracle/_ref, every core of this process, rank 0 only)."""
     import numpy as np
     import oracle as O
     px = dct_amd.synth(args.seed + 7, args.kind, 512, 512, device=dev)
@@ -257,7 +317,7 @@ def small_frame_leg(args, plan, dev):
     got = out.cpu().numpy()
     if O.ref_available():
         ref = np.zeros((4096, 64), np.int16)
-        threads = max(1, min(16, os.cpu_count() or 1))
+        threads = cpu_share()[0]
         reps, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < 1.0:
             O.ref().ref_forward_plane(np.ascontiguousarray(host).ravel(), 512, 512, args.quality, args.adaptive,
@@ -408,7 +468,8 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
     (_,), (r_other,) = other.round_trip_planes([luma[0]])
     psnr_other = psnr_of(r_other)
     bpb = 64 + 128 + 256
-    return {"op": "round_trip_planes (fused forward+inverse, one launch per step)", "steps": args.round_trip_steps,
+    return {"op": "round_trip_planes (fused forward+inverse, one launch per step; BASELINE configs[4])",
+            "world_size": world, "scaling": "weak", "frames_per_gpu": luma.shape[0], "steps": args.round_trip_steps,
             "blocks_per_s": world * nblk * args.round_trip_steps / el,
             "ms_per_step": el / args.round_trip_steps * 1e3,
             "bytes_per_block": bpb, "achieved_GBs_per_gpu": nblk * bpb * args.round_trip_steps / el / 1e9,
@@ -420,32 +481,88 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
                          "adaptive=1 with Q*(2-nv)"}
 
 
-def movement_ceiling_leg(plan, luma, chroma, coef_y, coef_c, rounds=10):
-    """Same-box memory ceiling of the forward kernel's access pattern:
-    dctq_diag_movement_planes moves exactly the bytes of the multi-plane forward
-    launch (same grid, prefetch, LDS stage, 1 KiB non-temporal stores) with no
-    arithmetic.  Interleaved with the real launch, HIP events, medians.  Writes
-    pixel bytes into coef_y/coef_c: run after the parity check (later legs
-    recompute their own outputs)."""
+def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10):
+    """Memory ceilings of the forward kernel's traffic on THIS box, interleaved
+    with the forward launch itself (HIP events, medians), through the diagnostic
+    library (libdct_amd_diag.so, csrc/dctq_diag.h):
+      movement_v2 : dctq_diag_movement_planes -- the forward launch's exact data
+                    movement (same grid, prefetch, LDS stage, 1 KiB stores), no math;
+      flat_1to2_* : dctq_diag_stream 0/1 -- the same byte counts as a flat stream
+                    (16 B per lane, 1 KiB per instruction), nt / default stores;
+      read_only / write_only : dctq_diag_stream 2/3 over the same byte counts;
+      phased      : read-only then write-only, i.e. the 1:2 traffic with no mix
+                    (not reachable by one launch that transforms the data:
+                    profiles/r02/hbm_ceilings.md).
+    movement_ceiling = the best of movement_v2 and the flat streams; the forward
+    kernel's time against it is forward_over_ceiling.  Overwrites coef_y/coef_c
+    (run after the parity check)."""
     import statistics
+    D = dct_amd.diag()
+    dplan = dct_amd.Plan(args.quality, args.adaptive, diagnostic=True)
     pls, outs = [luma, chroma], [coef_y, coef_c]
     nblk = coef_y.shape[0] + coef_c.shape[0]
-    tk, tm = [], []
+    nflat = nblk // 64 * 64
+    src = torch.empty(nflat * 64, dtype=torch.uint8, device=dev)
+    dst = torch.empty(nflat * 128, dtype=torch.uint8, device=dev)
+    src.fill_(7)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def diag_stream(kind):
+        rc = D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), nflat, stream)
+        if rc:
+            raise RuntimeError(f"dctq_diag_stream({kind}) rc={rc}")
+
+    cases = {
+        "forward": (lambda: plan.forward_quant_planes(pls, outs=outs), nblk * BYTES_PER_BLOCK),
+        "movement_v2": (lambda: dplan.diag_movement_planes(pls, outs), nblk * BYTES_PER_BLOCK),
+        "flat_1to2_nt_nt": (lambda: diag_stream(0), nflat * BYTES_PER_BLOCK),
+        "flat_1to2_nt_plain": (lambda: diag_stream(1), nflat * BYTES_PER_BLOCK),
+        "read_only": (lambda: diag_stream(2), nflat * 64),
+        "write_only": (lambda: diag_stream(3), nflat * 128),
+    }
+    times = {k: [] for k in cases}
     for r in range(rounds + 1):
-        for fn, acc in ((lambda: plan.forward_quant_planes(pls, outs=outs), tk),
-                        (lambda: plan.diag_movement_planes(pls, outs), tm)):
+        for k, (fn, _) in cases.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             fn()
             e1.record()
             torch.cuda.synchronize()
             if r:
-                acc.append(e0.elapsed_time(e1) * 1e-3)
-    k, m = statistics.median(tk), statistics.median(tm)
-    ach = BYTES_PER_BLOCK * nblk / m / 1e9
-    return {"kernel": "fdct8_movement (dctq_diag_movement_planes: same bytes, no arithmetic)",
-            "achieved": ach, "frac": ach / HBM_PEAK_GBS, "median_us": m * 1e6,
-            "forward_median_us": k * 1e6, "forward_over_ceiling": m / k, "rounds": rounds}
+                times[k].append(e0.elapsed_time(e1) * 1e-3)
+    med = {k: statistics.median(v) for k, v in times.items()}
+    frac = {k: cases[k][1] / med[k] / 1e9 / HBM_PEAK_GBS for k in cases}
+    phased = nflat * BYTES_PER_BLOCK / (med["read_only"] + med["write_only"]) / 1e9 / HBM_PEAK_GBS
+    best = max(("movement_v2", "flat_1to2_nt_nt", "flat_1to2_nt_plain"), key=lambda k: frac[k])
+    del src, dst
+    return {"pattern": best, "achieved": frac[best] * HBM_PEAK_GBS, "frac": frac[best],
+            "forward_frac": frac["forward"], "forward_over_ceiling": frac["forward"] / frac[best],
+            "forward_over_own_movement": frac["forward"] / frac["movement_v2"], "rounds": rounds,
+            "hw_ceilings": {**{k: {"median_us": med[k] * 1e6, "frac": frac[k]} for k in cases},
+                            "phased_read_then_write": {"frac": phased,
+                                                       "note": "two kernels: an upper bound no single launch "
+                                                               "that transforms the data reaches"}}}
+
+
+def traffic_for(args, launches):
+    """PMC HBM traffic of this exact configuration, or None with the reason: the
+    stored measurement (tools/pmc_traffic.py) must match frames, kind, quality,
+    adaptive mode, launches per step and the sha256 of the libdct_amd.so that
+    is loaded now."""
+    import hashlib
+    if not os.path.exists(args.traffic):
+        return None, "no profiles/traffic.json"
+    try:
+        tj = json.load(open(args.traffic))
+    except (OSError, ValueError) as e:
+        return None, f"unreadable traffic file: {e}"
+    lib_sha = hashlib.sha256(open(dct_amd.LIB_PATH, "rb").read()).hexdigest()
+    want = {"frames": args.frames, "kind": args.kind, "quality": args.quality, "adaptive": args.adaptive,
+            "launches_per_step": launches, "lib_sha256": lib_sha}
+    bad = [k for k, v in want.items() if tj.get(k) != v]
+    if bad:
+        return None, "stored PMC traffic does not match this run (" + ", ".join(bad) + ")"
+    return tj.get("bytes_per_launch"), "PMC FETCH_SIZE x 2 + WRITE_SIZE (tools/pmc_traffic.py)"
 
 
 def main():
@@ -462,6 +579,8 @@ def main():
             dist.init_process_group(args.backend)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
+    if world > 1:
+        world = dist.get_world_size()  # echo the process group's size, not only the launcher's env
     F = args.frames
     seed = args.seed + 100000 * rank
 
@@ -523,12 +642,12 @@ def main():
         nk = (C_W // 8) * (C_H // 8)
         fwd_check = (chroma[0].cpu().numpy(), coef_c[:nk].cpu().numpy())
 
-    movement = (movement_ceiling_leg(plan, luma, chroma, coef_y, coef_c, args.ceiling_rounds)
-                if args.ceiling_rounds > 0 else None)
+    movement = (ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, args.ceiling_rounds)
+                if args.ceiling_rounds > 0 and not args.per_plane else None)
 
     gather = band = None
     if world > 1 and args.gather_steps > 0:
-        gather = gather_leg(args, plan, luma, coef_y, world, rank, dev)
+        gather = gather_leg(args, plan, world, rank, dev)
         band = band_leg(args, plan, luma, chroma, world, dev)
 
     small = small_frame_leg(args, plan, dev) if world == 1 and not args.no_cpu else None  # single-GPU config
@@ -543,15 +662,7 @@ def main():
 
     total_blocks = world * (nblk_y + nblk_c) * args.steps
     value = total_blocks / el
-    traffic = None
-    if os.path.exists(args.traffic):
-        try:
-            tj = json.load(open(args.traffic))
-            if (tj.get("frames") == F and tj.get("kind") == args.kind
-                    and tj.get("launches_per_step", 2) == launches):
-                traffic = tj.get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_note = traffic_for(args, launches)
     if rank == 0:
         huf_check = encode["huffman"].pop("_check", None) if encode else None
         cpu, parity = (None, None) if args.no_cpu else cpu_leg(args, world, fwd_check, huf_check)
@@ -573,9 +684,10 @@ def main():
             "config": {"workload": f"4K 4:2:0 frame stream (BASELINE configs[2] planes), {F} frames/GPU/step, "
                                    f"forward DCT+quant q{args.quality} adaptive={args.adaptive}, int16 out",
                        "frames_per_gpu": F, "blocks_per_gpu_step": nblk_y + nblk_c, "quality": args.quality,
-                       "adaptive": args.adaptive, "parallelism": f"frames sharded over {world} GPU(s)"},
+                       "adaptive": args.adaptive, "parallelism": f"frames sharded over {world} GPU(s)",
+                       "world_size": world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": f"fdct8_quant_v2<{bool(args.adaptive)}, false, false>".lower(),
                          "avg_launch_us": avg_launch_s * 1e6, "launches_per_step": launches,
                          "bytes_per_launch": avg_launch_bytes, "movement_ceiling": movement},

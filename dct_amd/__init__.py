@@ -31,51 +31,73 @@ class _Plane(C.Structure):
 
 
 _lib = None
+_diag = None
+DIAG_PATH = os.path.join(HERE, "libdct_amd_diag.so")
+
+
+def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
+    vp, i, ll = C.c_void_p, C.c_int, C.c_longlong
+    sig = {
+        "dctq_plan_create": ([i, i, C.POINTER(vp)], i),
+        "dctq_plan_destroy": ([vp], None),
+        "dctq_plan_set_fallback_counter": ([vp, vp], i),
+        "dctq_forward_quant": ([vp, C.POINTER(_Plane), vp, vp, vp], i),
+        "dctq_forward_quant_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
+        "dctq_round_trip_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, vp], i),
+        "dctq_encode_workspace_bytes": ([ll], C.c_size_t),
+        "dctq_encode_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, ll, vp, vp], i),
+        "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
+        "dctq_inverse": ([vp, vp, vp, ll, vp, vp], i),
+        "dctq_synth": ([C.c_uint64, i, C.POINTER(_Plane), vp], i),
+        "dctq_error_string": ([i], C.c_char_p),
+        "dctq_synchronize": ([vp], i),
+        "dctq_rle_workspace_bytes": ([ll], C.c_size_t),
+        "dctq_rle_count": ([vp, ll, vp, vp, vp], i),
+        "dctq_rle_emit": ([vp, ll, vp, vp, vp], i),
+        "dctq_rle_decode": ([vp, vp, ll, vp, vp], i),
+        "dctq_huffman_bits": ([vp, ll, vp, vp], i),
+    }
+    if diagnostic:
+        sig.update({
+            "dctq_diag_plan_set_variant": ([vp, i], i),
+            "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
+            "dctq_diag_stream": ([i, vp, vp, ll, vp], i),
+            "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
+            "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
+            "dctq_debug_dc_table": ([i, vp], i),
+        })
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return L
 
 
 def lib() -> C.CDLL:
-    """Load libdct_amd.so (fails loudly if it has not been built)."""
+    """Load libdct_amd.so, the product library (fails loudly if it has not been built)."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise DctqError(f"{LIB_PATH} is missing: run `python -m dct_amd.build` (hipcc, gfx950)")
-        L = C.CDLL(LIB_PATH)
-        vp, i, ll = C.c_void_p, C.c_int, C.c_longlong
-        sig = {
-            "dctq_plan_create": ([i, i, C.POINTER(vp)], i),
-            "dctq_plan_destroy": ([vp], None),
-            "dctq_plan_set_fallback_counter": ([vp, vp], i),
-            "dctq_forward_quant": ([vp, C.POINTER(_Plane), vp, vp, vp], i),
-            "dctq_forward_quant_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
-            "dctq_round_trip_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, vp], i),
-            "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
-            "dctq_encode_workspace_bytes": ([ll], C.c_size_t),
-            "dctq_encode_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, ll, vp, vp], i),
-            "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
-            "dctq_inverse": ([vp, vp, vp, ll, vp, vp], i),
-            "dctq_synth": ([C.c_uint64, i, C.POINTER(_Plane), vp], i),
-            "dctq_error_string": ([i], C.c_char_p),
-            "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
-            "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
-            "dctq_debug_dc_table": ([i, vp], i),
-            "dctq_synchronize": ([vp], i),
-            "dctq_rle_workspace_bytes": ([ll], C.c_size_t),
-            "dctq_rle_count": ([vp, ll, vp, vp, vp], i),
-            "dctq_rle_emit": ([vp, ll, vp, vp, vp], i),
-            "dctq_rle_decode": ([vp, vp, ll, vp, vp], i),
-            "dctq_huffman_bits": ([vp, ll, vp, vp], i),
-        }
-        for name, (args, res) in sig.items():
-            fn = getattr(L, name)
-            fn.argtypes = args
-            fn.restype = res
-        _lib = L
+        _lib = _bind(C.CDLL(LIB_PATH), False)
     return _lib
 
 
-def _check(rc: int) -> None:
+def diag() -> C.CDLL:
+    """Load libdct_amd_diag.so: the same kernels plus the diagnostic entry points of
+    csrc/dctq_diag.h (test-only kernel selection, movement / hardware ceilings, host
+    table introspection).  Never used by the product path."""
+    global _diag
+    if _diag is None:
+        if not os.path.exists(DIAG_PATH):
+            raise DctqError(f"{DIAG_PATH} is missing: run `python -m dct_amd.build` (hipcc, gfx950)")
+        _diag = _bind(C.CDLL(DIAG_PATH), True)
+    return _diag
+
+
+def _check(rc: int, L: C.CDLL = None) -> None:
     if rc != 0:
-        raise DctqError(f"dctq error {rc}: {lib().dctq_error_string(rc).decode()}")
+        raise DctqError(f"dctq error {rc}: {(L or lib()).dctq_error_string(rc).decode()}")
 
 
 def _stream_ptr(stream=None):
@@ -102,15 +124,25 @@ class Plan:
     """Tables for one (quality, adaptive) configuration on the current device
     (quant_init(8, quality, adaptive) semantics, src/quantization.c:19-41)."""
 
-    def __init__(self, quality: int = 50, adaptive: bool = False):
+    def __init__(self, quality: int = 50, adaptive: bool = False, variant: int = None, diagnostic: bool = False):
+        """variant (tests / A/B only): force the forward kernel through the diagnostic
+        library (dctq_diag_plan_set_variant: 1 = v1, 3 = v3 in-place ties, 4 = v2 tie
+        queue, at any size); diagnostic: create the plan in the diagnostic library
+        (needed for diag_movement_planes)."""
         self.quality, self.adaptive = quality, bool(adaptive)
+        self._L = diag() if (variant is not None or diagnostic) else lib()
         h = C.c_void_p()
-        _check(lib().dctq_plan_create(int(quality), int(bool(adaptive)), C.byref(h)))
+        self._chk(self._L.dctq_plan_create(int(quality), int(bool(adaptive)), C.byref(h)))
         self._h = h
+        if variant is not None:
+            self._chk(self._L.dctq_diag_plan_set_variant(h, int(variant)))
+
+    def _chk(self, rc: int) -> None:
+        _check(rc, self._L)
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().dctq_plan_destroy(self._h)
+            self._L.dctq_plan_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -121,7 +153,7 @@ class Plan:
 
     def set_fallback_counter(self, counter):
         """counter: int64 CUDA tensor of one element (or None)."""
-        _check(lib().dctq_plan_set_fallback_counter(self._h, C.c_void_p(counter.data_ptr()) if counter is not None else None))
+        self._chk(self._L.dctq_plan_set_fallback_counter(self._h, C.c_void_p(counter.data_ptr()) if counter is not None else None))
 
     # --- hot path -------------------------------------------------------
     def forward_quant(self, px, out=None, var_num=None, stream=None):
@@ -131,7 +163,7 @@ class Plan:
         nblk = d.nframes * (d.width // 8) * (d.height // 8)
         if out is None:
             out = torch.empty((nblk, 64), dtype=torch.int16, device=px.device)
-        _check(lib().dctq_forward_quant(self._h, C.byref(d), C.c_void_p(out.data_ptr()),
+        self._chk(self._L.dctq_forward_quant(self._h, C.byref(d), C.c_void_p(out.data_ptr()),
                                         C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
                                         _stream_ptr(stream)))
         return out
@@ -147,7 +179,7 @@ class Plan:
                                 device=px.device) for d, px in zip(descs, planes)]
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         vp = (C.c_void_p * n)(*[v.data_ptr() for v in var_nums]) if var_nums is not None else None
-        _check(lib().dctq_forward_quant_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
+        self._chk(self._L.dctq_forward_quant_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
                                                C.cast(vp, C.c_void_p) if vp is not None else None,
                                                _stream_ptr(stream)))
         return outs
@@ -158,7 +190,9 @@ class Plan:
         n = len(planes)
         descs = (_Plane * n)(*[plane_desc(px) for px in planes])
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
-        _check(lib().dctq_diag_movement_planes(self._h, descs, n, C.cast(cp, C.c_void_p), _stream_ptr(stream)))
+        if self._L is not _diag:
+            raise DctqError("diag_movement_planes needs a plan of the diagnostic library (Plan(..., diagnostic=True))")
+        self._chk(self._L.dctq_diag_movement_planes(self._h, descs, n, C.cast(cp, C.c_void_p), _stream_ptr(stream)))
         return outs
 
     def round_trip_planes(self, planes, outs=None, recons=None, var_nums=None, stream=None):
@@ -176,7 +210,7 @@ class Plan:
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         rp = (C.c_void_p * n)(*[r.data_ptr() for r in recons])
         vp = (C.c_void_p * n)(*[v.data_ptr() for v in var_nums]) if var_nums is not None else None
-        _check(lib().dctq_round_trip_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
+        self._chk(self._L.dctq_round_trip_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
                                             C.cast(vp, C.c_void_p) if vp is not None else None,
                                             C.cast(rp, C.c_void_p), _stream_ptr(stream)))
         return outs, recons
@@ -197,9 +231,9 @@ class Plan:
         cap = 64 * nb if capacity is None else int(capacity)
         off = torch.empty(nb + 1, dtype=torch.int32, device=dev)
         sym = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
-        ws = torch.empty(int(lib().dctq_encode_workspace_bytes(nb)) // 4 + 1, dtype=torch.int32, device=dev)
+        ws = torch.empty(int(self._L.dctq_encode_workspace_bytes(nb)) // 4 + 1, dtype=torch.int32, device=dev)
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
-        _check(lib().dctq_encode_planes(self._h, descs, n, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
+        self._chk(self._L.dctq_encode_planes(self._h, descs, n, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
                                         C.c_void_p(sym.data_ptr()), cap, C.c_void_p(ws.data_ptr()),
                                         _stream_ptr(stream)))
         total = int(off[nb].item()) & 0xFFFFFFFF
@@ -211,7 +245,7 @@ class Plan:
         nblk = d.nframes * (d.width // 8) * (d.height // 8)
         if out is None:
             out = torch.empty((nblk, 64), dtype=torch.float32, device=px.device)
-        _check(lib().dctq_forward_float(self._h, C.byref(d), C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+        self._chk(self._L.dctq_forward_float(self._h, C.byref(d), C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
         return out
 
     def inverse(self, coef, var_num=None, out=None, stream=None):
@@ -220,7 +254,7 @@ class Plan:
         n = coef.numel() // 64
         if out is None:
             out = torch.empty((n, 64), dtype=torch.float32, device=coef.device)
-        _check(lib().dctq_inverse(self._h, C.c_void_p(coef.data_ptr()),
+        self._chk(self._L.dctq_inverse(self._h, C.c_void_p(coef.data_ptr()),
                                   C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
                                   n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
         return out
@@ -285,6 +319,6 @@ def debug_tables(quality: int, adaptive: bool = False):
     thr = np.zeros(64, np.float32)
     d = np.zeros(64, np.float64)
     q = np.zeros(64, np.float64)
-    _check(lib().dctq_debug_tables(quality, int(adaptive), w.ctypes.data, thr.ctypes.data, d.ctypes.data,
-                                   q.ctypes.data))
+    _check(diag().dctq_debug_tables(quality, int(adaptive), w.ctypes.data, thr.ctypes.data, d.ctypes.data,
+                                    q.ctypes.data))
     return w, thr, d, q

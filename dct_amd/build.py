@@ -2,16 +2,22 @@
 
     python -m dct_amd.build            # or dct_amd.build.build()
 
-Explicit hipcc lines (one object per source, compiled in parallel, then one
-link) -- no torch extension machinery: the library is a plain
+Explicit hipcc lines (one object per source, compiled in parallel, then two
+links) -- no torch extension machinery: the library is a plain
 C-ABI shared object that a C host links with -ldct_amd and Python loads with
-ctypes.  -ffp-contract=off is load-bearing (DESIGN.md "Exactness"): the exact
+ctypes.  Two libraries come out of the same objects:
+  libdct_amd.so       the product: exports exactly the functions declared in
+                      include/*.h (a version script generated from them);
+  libdct_amd_diag.so  + diag.hip: the diagnostic entry points of
+                      csrc/dctq_diag.h (kernel selection for tests, movement and
+                      hardware ceilings for bench.py, host table introspection).  -ffp-contract=off is load-bearing (DESIGN.md "Exactness"): the exact
 tie path must not fuse multiply-add, and the fast path asks for every FMA it
 wants explicitly.
 """
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 import sys
 
@@ -19,16 +25,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdct_amd.so")
+DIAG_LIB = os.path.join(HERE, "libdct_amd_diag.so")
+DIAG_SOURCES = ["diag.hip"]
 SOURCES = ["api.hip", "legacy.hip", "fdct8.hip", "fdct8_aux.hip", "f64_pair.hip", "rle.hip", "roundtrip.hip", "encode.hip", "huffman.hip"]
-HEADERS = ["dctq_internal.h", "fdct8_bound.h", "host_tables.h", "aan_f64.h", "fdct8_core.h", "pair_core.h", "scan_core.h", "zigzag.h"]
+HEADERS = ["dctq_internal.h", "plan.h", "dctq_diag.h", "fdct8_bound.h", "host_tables.h", "aan_f64.h", "fdct8_core.h", "pair_core.h", "scan_core.h", "zigzag.h"]
 ARCH = "gfx950"
 
 
 def _stale() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(DIAG_LIB):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
+    t = min(os.path.getmtime(LIB), os.path.getmtime(DIAG_LIB))
+    deps = [os.path.join(CSRC, f) for f in SOURCES + DIAG_SOURCES + HEADERS] + [__file__]
     deps += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
     return any(os.path.getmtime(d) > t for d in deps)
 
@@ -39,35 +47,61 @@ def _flags():
             "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
 
+def declared_functions(headers) -> list:
+    """C function names declared in the given headers (comments stripped)."""
+    names = set()
+    for h in headers:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\(", src, flags=re.M):
+            if m.group(1) not in ("if", "while", "for", "return", "sizeof", "defined"):
+                names.add(m.group(1))
+    return sorted(names)
+
+
+def public_headers() -> list:
+    inc = os.path.join(ROOT, "include")
+    return [os.path.join(inc, f) for f in sorted(os.listdir(inc)) if f.endswith(".h")]
+
+
+def _version_script(path: str, names) -> str:
+    with open(path, "w") as f:
+        f.write("{\n  global:\n" + "".join(f"    {n};\n" for n in names) + "  local: *;\n};\n")
+    return path
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile each source to an object in parallel (dct_amd/_obj/), then link the .so."""
+    """Compile each source to an object in parallel (dct_amd/_obj/), then link both libraries."""
     if not force and not _stale():
         return LIB
     from concurrent.futures import ThreadPoolExecutor
     objdir = os.path.join(HERE, "_obj")
     os.makedirs(objdir, exist_ok=True)
-    objs = [os.path.join(objdir, os.path.splitext(src)[0] + ".o") for src in SOURCES]
+    srcs = SOURCES + DIAG_SOURCES
+    objs = {src: os.path.join(objdir, os.path.splitext(src)[0] + ".o") for src in srcs}
 
-    def compile_one(src_obj):
-        src, obj = src_obj
-        cmd = _flags() + ["-c", os.path.join(CSRC, src), "-o", obj]
+    def compile_one(src):
+        cmd = _flags() + ["-c", os.path.join(CSRC, src), "-o", objs[src]]
         if verbose:
             print(" ".join(cmd))
         return subprocess.run(cmd, capture_output=True, text=True)
 
-    jobs = min(len(SOURCES), max(1, min(16, os.cpu_count() or 1)))
+    jobs = min(len(srcs), max(1, min(16, os.cpu_count() or 1)))
     with ThreadPoolExecutor(jobs) as ex:
-        results = list(ex.map(compile_one, zip(SOURCES, objs)))
-    for src, out in zip(SOURCES, results):
+        results = list(ex.map(compile_one, srcs))
+    for src, out in zip(srcs, results):
         if out.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n" + out.stdout + out.stderr)
-    cmd = _flags() + ["-shared", *objs, "-o", LIB + ".tmp"]
-    if verbose:
-        print(" ".join(cmd))
-    out = subprocess.run(cmd, capture_output=True, text=True)
-    if out.returncode != 0:
-        raise RuntimeError("hipcc link failed:\n" + out.stdout + out.stderr)
-    os.replace(LIB + ".tmp", LIB)
+    pub = declared_functions(public_headers())
+    diag = declared_functions(public_headers() + [os.path.join(CSRC, "dctq_diag.h")])
+    for lib, names, parts in ((LIB, pub, SOURCES), (DIAG_LIB, diag, srcs)):
+        vs = _version_script(os.path.join(objdir, os.path.basename(lib) + ".map"), names)
+        cmd = _flags() + ["-shared", *[objs[s_] for s_ in parts], f"-Wl,--version-script={vs}", "-o", lib + ".tmp"]
+        if verbose:
+            print(" ".join(cmd))
+        out = subprocess.run(cmd, capture_output=True, text=True)
+        if out.returncode != 0:
+            raise RuntimeError("hipcc link failed:\n" + out.stdout + out.stderr)
+        os.replace(lib + ".tmp", lib)
     return LIB
 
 

@@ -17,21 +17,14 @@
 #include "dctq_internal.h"
 #include "fdct8_bound.h"
 #include "host_tables.h"
-
-struct dctq_plan {
-    int quality, adaptive, device, num_cus, variant;
-    dctq::FastTables fast;       // thresholds for the mode in `adaptive`
-    dctq::DevTables host;        // host copy of the device tables
-    dctq::DevTables *dev;        // device copy
-    unsigned long long *fallbacks;
-    void *ring;                  // v2 tie-path pixel stash (one stream at a time per plan)
-    int ring_wgs;                // workgroups the stash is sized for
-};
+#include "plan.h"
 
 namespace {
 thread_local std::string g_err;
+}  // namespace
 
-int fail(int code, const char *what, hipError_t e = hipSuccess) {
+namespace dctq {
+int fail(int code, const char *what, hipError_t e) {
     g_err = what;
     if (e != hipSuccess) {
         g_err += ": ";
@@ -39,12 +32,8 @@ int fail(int code, const char *what, hipError_t e = hipSuccess) {
     }
     return code;
 }
-#define HIPCHK(call, what)                                  \
-    do {                                                    \
-        hipError_t e_ = (call);                             \
-        if (e_ != hipSuccess) return fail(DCTQ_EHIP, what, e_); \
-    } while (0)
-}  // namespace
+}  // namespace dctq
+using dctq::fail;
 
 namespace dctq {
 FastDiv make_fastdiv(uint32_t d) {
@@ -95,7 +84,7 @@ void fill_fast_tables(const double *q, int adaptive, FastTables *t) {
 // temp[k][0] = sum_l x * D[0][l] (the same for every row k, l ascending), then
 // out = sum_k D[0][k] * temp[k][0], q = (int) round(out / Q[0]).  This file is
 // compiled with -ffp-contract=off, so host arithmetic is the reference's.
-static void dc_const_table(const double *d, const double *q, int16_t *tab) {
+void dctq::dc_const_table(const double *d, const double *q, int16_t *tab) {
     for (int v = 0; v < 256; ++v) {
         const double x = (double)v - 128.0;
         double t = 0.0;
@@ -121,8 +110,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
     p->adaptive = adaptive ? 1 : 0;
     p->device = dev;
     p->num_cus = prop.multiProcessorCount;
-    p->variant = 2;
-    if (const char *v = getenv("DCTQ_FDCT_VARIANT")) p->variant = atoi(v);
+    p->variant = 2;  // dispatch by launch size (fdct8.hip); the diagnostic library can force another
     p->fallbacks = nullptr;
     dctq_host::dct_matrix(8, p->host.dct);
     for (int c = 0; c < 64; ++c) {
@@ -134,7 +122,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
         p->host.qscale[c] = q[c] * s2;
     }
     dctq::fill_fast_tables(q, p->adaptive, &p->fast);
-    dc_const_table(p->host.dct, p->host.quant, p->host.dc_const);
+    dctq::dc_const_table(p->host.dct, p->host.quant, p->host.dc_const);
     for (int k = 0; k < 8; ++k) p->host.s1[k] = kAanScale[k];
     p->host.fast = p->fast;
     hipError_t e = hipMalloc(&p->dev, sizeof(dctq::DevTables));
@@ -159,7 +147,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
     return DCTQ_OK;
 }
 
-static int plane_args(const dctq_plane *s, dctq::PlaneArgs *a) {
+int dctq::plane_args(const dctq_plane *s, dctq::PlaneArgs *a) {
     if (!s || !s->pixels) return fail(DCTQ_EINVAL, "plane/pixels is NULL");
     if (s->width <= 0 || s->height <= 0 || s->width % 8 || s->height % 8)
         return fail(DCTQ_EINVAL, "width and height must be positive multiples of 8");
@@ -242,8 +230,10 @@ int dctq_plan_set_fallback_counter(dctq_plan *plan, unsigned long long *counter)
     return DCTQ_OK;
 }
 
+}  // extern "C"
+
 // A plan's tables and stash live on the device that was current at its creation.
-static int check_plan(const dctq_plan *plan) {
+int dctq::check_plan(const dctq_plan *plan) {
     if (!plan) return fail(DCTQ_EINVAL, "plan is NULL");
     int dev = -1;
     HIPCHK(hipGetDevice(&dev), "hipGetDevice");
@@ -251,8 +241,8 @@ static int check_plan(const dctq_plan *plan) {
     return DCTQ_OK;
 }
 
-static int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num,
-                     dctq::PlaneSet *ps_out) {
+int dctq::plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num,
+                    dctq::PlaneSet *ps_out) {
     if (!planes || !coef) return fail(DCTQ_EINVAL, "planes/coef is NULL");
     if (nplanes < 1 || nplanes > dctq::kMaxPlanes) return fail(DCTQ_EINVAL, "nplanes must be in [1, 4]");
     dctq::PlaneSet &ps = *ps_out;
@@ -263,7 +253,7 @@ static int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef
         if (!coef[k]) return fail(DCTQ_EINVAL, "coef[k] is NULL");
         if (((uintptr_t)coef[k]) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
         if (var_num && !var_num[k]) return fail(DCTQ_EINVAL, "var_num given but var_num[k] is NULL");
-        int rc = plane_args(&planes[k], &ps.pl[k]);
+        int rc = dctq::plane_args(&planes[k], &ps.pl[k]);
         if (rc) return rc;
         ps.coef[k] = coef[k];
         ps.var[k] = var_num ? var_num[k] : nullptr;
@@ -275,12 +265,14 @@ static int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef
     return DCTQ_OK;
 }
 
+extern "C" {
+
 int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               int32_t *const *var_num, void *stream) {
     DCTQ_ENTRY;
-    if (int rc = check_plan(plan)) return rc;
+    if (int rc = dctq::check_plan(plan)) return rc;
     dctq::PlaneSet ps;
-    int rc = plane_set(planes, nplanes, coef, var_num, &ps);
+    int rc = dctq::plane_set(planes, nplanes, coef, var_num, &ps);
     if (rc) return rc;
     HIPCHK(dctq::launch_fdct8_quant(ps, plan->fast, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
                                     plan->variant, plan->num_cus, plan->ring, plan->ring_wgs),
@@ -288,24 +280,13 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
     return DCTQ_OK;
 }
 
-int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
-                              void *stream) {
-    DCTQ_ENTRY;
-    if (int rc = check_plan(plan)) return rc;
-    dctq::PlaneSet ps;
-    int rc = plane_set(planes, nplanes, coef, nullptr, &ps);
-    if (rc) return rc;
-    HIPCHK(dctq::launch_fdct8_movement(ps, (hipStream_t)stream, plan->num_cus), "fdct8_movement launch");
-    return DCTQ_OK;
-}
-
 int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                            int32_t *const *var_num, float *const *recon, void *stream) {
     DCTQ_ENTRY;
-    if (int rc = check_plan(plan)) return rc;
+    if (int rc = dctq::check_plan(plan)) return rc;
     if (!recon) return fail(DCTQ_EINVAL, "recon is NULL");
     dctq::RoundTripSet rt = {};
-    int rc = plane_set(planes, nplanes, coef, var_num, &rt.ps);
+    int rc = dctq::plane_set(planes, nplanes, coef, var_num, &rt.ps);
     if (rc) return rc;
     for (int k = 0; k < nplanes; ++k) {
         if (!recon[k] || ((uintptr_t)recon[k]) % 16) return fail(DCTQ_EINVAL, "recon[k] NULL or not 16-byte aligned");
@@ -324,11 +305,11 @@ int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int npla
                        uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
                        void *stream) {
     DCTQ_ENTRY;
-    if (int rc = check_plan(plan)) return rc;
+    if (int rc = dctq::check_plan(plan)) return rc;
     if (!offsets || !workspace) return fail(DCTQ_EINVAL, "offsets/workspace is NULL");
     if (symbols_capacity < 0) return fail(DCTQ_EINVAL, "symbols_capacity < 0");
     dctq::EncodeSet es = {};
-    int rc = plane_set(planes, nplanes, coef, nullptr, &es.ps);
+    int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &es.ps);
     if (rc) return rc;
     long long blocks = 0;
     for (int k = 0; k < nplanes; ++k) {
@@ -352,11 +333,11 @@ int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *co
 
 int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream) {
     DCTQ_ENTRY;
-    if (int rc = check_plan(plan)) return rc;
+    if (int rc = dctq::check_plan(plan)) return rc;
     if (!coef) return fail(DCTQ_EINVAL, "coef is NULL");
     if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
     dctq::PlaneArgs a;
-    int rc = plane_args(src, &a);
+    int rc = dctq::plane_args(src, &a);
     if (rc) return rc;
     if (plan->variant == 1)
         HIPCHK(dctq::launch_fdct8_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
@@ -369,7 +350,7 @@ int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef
 int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks, float *recon,
                  void *stream) {
     DCTQ_ENTRY;
-    if (int rc = check_plan(plan)) return rc;
+    if (int rc = dctq::check_plan(plan)) return rc;
     if (!coef || !recon) return fail(DCTQ_EINVAL, "coef/recon is NULL");
     if (plan->adaptive && !var_num) return fail(DCTQ_EINVAL, "adaptive inverse needs var_num");
     if (nblocks < 0 || nblocks >= (1ll << 40)) return fail(DCTQ_EINVAL, "bad nblocks");
@@ -496,33 +477,6 @@ const char *dctq_error_string(int code) {
     case DCTQ_ENODEV: return "no gfx950 device";
     default: return "unknown error";
     }
-}
-
-/* Introspection for tests (host-only, no GPU needed): the tables a plan would use. */
-int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *dct, double *quant) {
-    double q[64];
-    quality = dctq_host::clamp_quality(quality);
-    dctq_host::quant_matrix(8, quality, q);
-    dctq::FastTables t;
-    dctq::fill_fast_tables(q, adaptive, &t);
-    if (w) memcpy(w, t.w, sizeof t.w);
-    if (thr) memcpy(thr, t.thr, sizeof t.thr);
-    if (dct) dctq_host::dct_matrix(8, dct);
-    if (quant) memcpy(quant, q, sizeof q);
-    return DCTQ_OK;
-}
-
-int dctq_debug_dc_table(int quality, int16_t *out) {
-    double d[64], q[64];
-    dctq_host::dct_matrix(8, d);
-    dctq_host::quant_matrix(8, dctq_host::clamp_quality(quality), q);
-    dc_const_table(d, q, out);
-    return DCTQ_OK;
-}
-
-int dctq_debug_fastdiv(uint32_t d, uint32_t n) {
-    dctq::FastDiv f = dctq::make_fastdiv(d);
-    return (int)((((uint64_t)n * f.m >> 32) + n) >> f.s);
 }
 
 }  // extern "C"

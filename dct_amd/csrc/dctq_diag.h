@@ -1,0 +1,47 @@
+/* dct_amd/csrc/dctq_diag.h -- the C-ABI of libdct_amd_diag.so, the DIAGNOSTIC
+ * build of this library: the same objects as libdct_amd.so plus diag.hip.  Not
+ * a codec surface (no include/ header): measurement (bench.py's ceilings, the
+ * A/B tools) and test-only controls.  Every product entry point of
+ * include/dct_amd.h is exported by this library too, so a plan created here can
+ * be used with any of them -- but a plan belongs to the library that created it. */
+#ifndef DCTQ_DIAG_H
+#define DCTQ_DIAG_H
+
+#include "dct_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Force the forward kernel of a plan (test-only; libdct_amd.so picks by launch
+ * size): 2 = the product dispatch, 1 = v1 (one workgroup per 256 blocks), 3 =
+ * v3 (in-place ties) at any size, 4 = v2 (tie queue) at any size.  Also routes
+ * dctq_forward_float / dctq_inverse to their lane-per-block kernels when 1. */
+int dctq_diag_plan_set_variant(dctq_plan *plan, int variant);
+
+/* Moves exactly the bytes dctq_forward_quant_planes moves (same grid, prefetch,
+ * LDS stage and 1 KiB stores) with no arithmetic.  coef[k] receives pixel bytes,
+ * NOT coefficients.  Its time is the memory ceiling of the forward kernel's own
+ * access pattern. */
+int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                              void *stream);
+
+/* Hardware ceilings of the forward kernel's traffic (64 B read : 128 B written
+ * per block), independent of its access pattern (profiles/r02/hbm_ceilings.md):
+ *   kind 0: flat 1:2 stream, per wave 4 x 1 KiB loads then 8 x 1 KiB stores per
+ *           64-block batch, persistent grid, nt loads, nt stores;
+ *   kind 1: the same with default-policy stores;
+ *   kind 2: read-only stream of blocks * 64 bytes of src (nt);
+ *   kind 3: write-only stream of blocks * 128 bytes of dst (default policy).
+ * src >= blocks * 64 bytes, dst >= blocks * 128 bytes, both 16-byte aligned. */
+int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
+
+/* Host-only introspection for the CPU tests (no GPU needed). */
+int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *dct, double *quant);
+int dctq_debug_dc_table(int quality, int16_t *out);
+int dctq_debug_fastdiv(uint32_t d, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

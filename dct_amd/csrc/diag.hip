@@ -1,0 +1,137 @@
+// dct_amd/csrc/diag.hip -- the diagnostic entry points of libdct_amd_diag.so
+// (dctq_diag.h): kernel selection for tests, the forward kernel's movement
+// ceiling, the hardware ceilings of its traffic mix, and host-only table
+// introspection.  Linked into the diagnostic library only; libdct_amd.so (the
+// product) neither contains nor exports any of it.
+#include <string.h>
+
+#include "dctq_diag.h"
+#include "host_tables.h"
+#include "plan.h"
+
+namespace dctq {
+namespace {
+
+typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+
+// Flat 1:2 stream (profiles/r02/hbm_ceilings.md "s12"): wave-batch b reads
+// src[4 KiB * b, +4 KiB) with 4 x 16-B-per-lane loads and writes
+// dst[8 KiB * b, +8 KiB) with 8 x 1 KiB stores.  AUX = store policy.
+template <int AUX>
+__global__ __launch_bounds__(256) void stream12(const u4v *__restrict__ src, char *__restrict__ dst, uint32_t nb) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < nb; b += gridDim.x * 4) {
+        u4v v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(src + (size_t)b * 256 + k * 64 + lane);
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 8192, 0, 8192, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            __builtin_amdgcn_raw_buffer_store_b128(v[k], rc, lane * 16, k * 1024, AUX);
+            __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{1, 0, 0, 0}, rc, lane * 16, (k + 4) * 1024, AUX);
+        }
+    }
+}
+
+// read-only: 4 x 16 B per thread, xor-reduced (the store never happens)
+__global__ __launch_bounds__(256) void stream_read(const u4v *__restrict__ src, u4v *__restrict__ sink, size_t n16) {
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+    u4v acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (base + u * 256 < n16) acc ^= __builtin_nontemporal_load(src + base + u * 256);
+    if (acc.x == 0x12345678u && acc.y == 0x9abcdef0u && acc.z == 0x0fedcba9u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void stream_write(u4v *__restrict__ dst, size_t n16) {
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        if (base + u * 256 < n16) dst[base + u * 256] = u4v{(unsigned)base, (unsigned)u, 7u, 9u};
+}
+
+int device_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) return 256;
+    return n;
+}
+
+}  // namespace
+}  // namespace dctq
+
+extern "C" {
+
+int dctq_diag_plan_set_variant(dctq_plan *plan, int variant) {
+    DCTQ_ENTRY;
+    if (!plan) return dctq::fail(DCTQ_EINVAL, "plan is NULL");
+    if (variant < 1 || variant > 4) return dctq::fail(DCTQ_EINVAL, "variant must be 1..4");
+    plan->variant = variant;
+    return DCTQ_OK;
+}
+
+int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                              void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = dctq::check_plan(plan)) return rc;
+    dctq::PlaneSet ps;
+    if (int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &ps)) return rc;
+    HIPCHK(dctq::launch_fdct8_movement(ps, (hipStream_t)stream, plan->num_cus), "fdct8_movement launch");
+    return DCTQ_OK;
+}
+
+int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream) {
+    DCTQ_ENTRY;
+    using namespace dctq;
+    if (!src || !dst || ((uintptr_t)src) % 16 || ((uintptr_t)dst) % 16) return fail(DCTQ_EINVAL, "src/dst NULL or misaligned");
+    if (blocks < 64 || blocks % 64 || blocks >= (1ll << 31)) return fail(DCTQ_EINVAL, "blocks must be a multiple of 64 in [64, 2^31)");
+    const uint32_t nb = (uint32_t)(blocks / 64);
+    const hipStream_t s = (hipStream_t)stream;
+    const int grid = device_cus() * 4;
+    switch (kind) {
+    case 0: hipLaunchKernelGGL(stream12<2>, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
+    case 1: hipLaunchKernelGGL(stream12<0>, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
+    case 2: {
+        const size_t n16 = (size_t)blocks * 4;
+        hipLaunchKernelGGL(stream_read, dim3((unsigned)((n16 + 1023) / 1024)), dim3(256), 0, s, (const u4v *)src,
+                           (u4v *)dst, n16);
+        break;
+    }
+    case 3: {
+        const size_t n16 = (size_t)blocks * 8;
+        hipLaunchKernelGGL(stream_write, dim3((unsigned)((n16 + 1023) / 1024)), dim3(256), 0, s, (u4v *)dst, n16);
+        break;
+    }
+    default: return fail(DCTQ_EINVAL, "kind must be 0..3");
+    }
+    HIPCHK(hipGetLastError(), "diag stream launch");
+    return DCTQ_OK;
+}
+
+int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *dct, double *quant) {
+    double q[64];
+    quality = dctq_host::clamp_quality(quality);
+    dctq_host::quant_matrix(8, quality, q);
+    dctq::FastTables t;
+    dctq::fill_fast_tables(q, adaptive, &t);
+    if (w) memcpy(w, t.w, sizeof t.w);
+    if (thr) memcpy(thr, t.thr, sizeof t.thr);
+    if (dct) dctq_host::dct_matrix(8, dct);
+    if (quant) memcpy(quant, q, sizeof q);
+    return DCTQ_OK;
+}
+
+int dctq_debug_dc_table(int quality, int16_t *out) {
+    double d[64], q[64];
+    dctq_host::dct_matrix(8, d);
+    dctq_host::quant_matrix(8, dctq_host::clamp_quality(quality), q);
+    dctq::dc_const_table(d, q, out);
+    return DCTQ_OK;
+}
+
+int dctq_debug_fastdiv(uint32_t d, uint32_t n) {
+    dctq::FastDiv f = dctq::make_fastdiv(d);
+    return (int)((((uint64_t)n * f.m >> 32) + n) >> f.s);
+}
+
+}  // extern "C"

@@ -1,0 +1,35 @@
+// dct_amd/csrc/plan.h -- the plan object and the argument helpers shared by the
+// product C-ABI (api.hip) and the diagnostic library's entry points (diag.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dct_amd.h"
+#include "dctq_internal.h"
+
+struct dctq_plan {
+    int quality, adaptive, device, num_cus;
+    int variant;                 // 2: dispatch by launch size; others only via libdct_amd_diag.so
+    dctq::FastTables fast;       // thresholds for the mode in `adaptive`
+    dctq::DevTables host;        // host copy of the device tables
+    dctq::DevTables *dev;        // device copy
+    unsigned long long *fallbacks;
+    void *ring;                  // v2 tie-path pixel stash (one stream at a time per plan)
+    int ring_wgs;                // workgroups the stash is sized for
+};
+
+namespace dctq {
+// records `what` (+ the HIP error string) for dctq_error_string and returns `code`
+int fail(int code, const char *what, hipError_t e = hipSuccess);
+int check_plan(const dctq_plan *plan);
+int plane_args(const dctq_plane *s, PlaneArgs *a);
+int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num, PlaneSet *ps);
+void fill_fast_tables(const double *q, int adaptive, FastTables *t);
+// quantized DC of every constant block, in the reference's operation order (api.hip)
+void dc_const_table(const double *d, const double *q, int16_t *tab);
+}  // namespace dctq
+
+#define HIPCHK(call, what)                                               \
+    do {                                                                 \
+        hipError_t e_ = (call);                                          \
+        if (e_ != hipSuccess) return ::dctq::fail(DCTQ_EHIP, what, e_); \
+    } while (0)

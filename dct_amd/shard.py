@@ -127,3 +127,46 @@ def gather_symbols(offsets, symbols, group=None):
         base += tr
     offs.append(torch.tensor([base], dtype=torch.int64, device=dev))
     return torch.cat(offs).to(torch.int32), torch.cat(syms)
+
+
+def max_over_ranks(seconds: float, device, group=None) -> float:
+    """Wall time of a timed region as the job sees it: the slowest rank's."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
+
+
+def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: None, group=None) -> dict:
+    """BASELINE configs[3]: a fixed batch of frames split over the ranks
+    (strong scaling; `frames` is this rank's frame_shard), forward DCT+quant of
+    the shard, then the coefficient planes all-gathered onto every rank.
+
+    forward(frames) -> int16 [counts[rank], 64] (the device kernel on the GPU,
+    anything equivalent in the CPU tests); `sync` waits for the device.  Two
+    timed loops of `steps` steps, each bracketed by a barrier and `sync`, the
+    time the max over ranks:
+      kernel-only : forward alone -> the aggregate rate of the GPUs' kernels;
+      end-to-end  : forward + gather_coefficients -> what a caller that needs
+                    every coefficient on every rank gets (xGMI-bound).
+    Returns the two times, the blocks per step and the last gathered tensor."""
+    import time
+    import torch.distributed as dist
+    total = sum(counts)
+
+    def timed(fn):
+        out = fn()
+        sync()
+        dist.barrier(group=group)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = fn()
+        sync()
+        return max_over_ranks(time.perf_counter() - t0, device, group), out
+
+    t_kernel, local = timed(lambda: forward(frames))
+    t_e2e, full = timed(lambda: gather_coefficients(forward(frames), counts, group))
+    return {"blocks_per_step": total, "steps": steps, "kernel_s": t_kernel, "end_to_end_s": t_e2e,
+            "local": local, "full": full}

@@ -74,14 +74,6 @@ int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *co
 int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               int32_t *const *var_num, void *stream);
 
-/* DIAGNOSTIC, not a codec call: moves exactly the bytes dctq_forward_quant_planes
- * moves (same grid, prefetch, LDS stage and 1 KiB stores) with no arithmetic.
- * coef[k] receives pixel bytes, NOT coefficients.  Its time is the memory
- * ceiling of the forward kernel's access pattern on the running device
- * (bench.py reports kernel time against it). */
-int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
-                              void *stream);
-
 /* Fused round trip (BASELINE configs[4]) of up to 4 planes in ONE launch: for
  * plane k, coef[k] (and var_num[k] if var_num is non-NULL) exactly as
  * dctq_forward_quant_planes, and

@@ -86,16 +86,17 @@ def ref_available() -> bool:
     return os.path.exists(_REF)
 
 
-_ref = None
+_refs = {}
 
 
-def ref():
-    """The compiled reference (oracle/_ref/libref.so)."""
-    global _ref
-    if _ref is None:
-        if not os.path.exists(_REF):
-            raise FileNotFoundError(_REF + " (run `make -C oracle` where /root/reference exists)")
-        lib = C.CDLL(_REF)
+def ref(build: str = "O2"):
+    """The compiled reference: oracle/_ref/libref.so (Justfile flags + -O2) or, with
+    build="O0", oracle/_ref/libref_O0.so (the Justfile flags as they are: -g, -O0)."""
+    path = _REF if build == "O2" else _REF.replace("libref.so", "libref_O0.so")
+    if build not in _refs:
+        if not os.path.exists(path):
+            raise FileNotFoundError(path + " (run `make -C oracle` where /root/reference exists)")
+        lib = C.CDLL(path)
         lib.ref_dct_matrix.argtypes = [C.c_int, _dp]
         lib.ref_quant_tables.argtypes = [C.c_int, C.c_int, C.c_int, _dp, _dp, C.POINTER(C.c_int)]
         lib.ref_forward.argtypes = [C.c_int, _dp, _dp]
@@ -113,8 +114,8 @@ def ref():
         lib.ref_forward_plane.restype = C.c_long
         lib.ref_huffman_bits.argtypes = [C.c_int, _ip, C.POINTER(C.c_int), C.POINTER(C.c_int)]
         lib.ref_huffman_bits.restype = C.c_int
-        _ref = lib
-    return _ref
+        _refs[build] = lib
+    return _refs[build]
 
 
 # ---------------------------------------------------------------- oracle API

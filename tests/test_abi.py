@@ -21,15 +21,13 @@ def lib():
 
 
 def declared_functions():
-    names = set()
-    for h in os.listdir(os.path.join(ROOT, "include")):
-        src = open(os.path.join(ROOT, "include", h)).read()
-        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b([a-z_][a-z0-9_]*)\s*\(", src, flags=re.M):
-            name = m.group(1)
-            if name not in ("if", "while", "for", "return", "sizeof", "defined"):
-                names.add(name)
-    return names
+    from dct_amd.build import declared_functions as dec, public_headers
+    return set(dec(public_headers()))
+
+
+def exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if " T " in l}
 
 
 def test_every_declared_symbol_exported(lib):
@@ -40,13 +38,32 @@ def test_every_declared_symbol_exported(lib):
                "generate_dequant_matrix", "quantize", "dequantize", "calculate_block_variance",
                "adjust_matrix_for_block", "alloc_array", "free_array", "alloc_int_array", "free_int_array"}
     assert ref_api <= names, ref_api - names
+    # the product library exports exactly what include/*.h declares: no diagnostics, no internals
+    got = exported(os.path.join(ROOT, "dct_amd", "libdct_amd.so"))
+    assert got == names, (names - got, got - names)
     out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "dct_amd", "libdct_amd.so")],
                          capture_output=True, text=True).stdout
-    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
-    missing = names - exported
-    assert not missing, missing
+    assert not [l for l in out.splitlines() if " T " not in l and " A " not in l], "non-function exports"
     for n in names:
         getattr(lib, n)
+
+
+def test_diagnostic_library_exports(lib):
+    """libdct_amd_diag.so = the product's exports + exactly csrc/dctq_diag.h."""
+    from dct_amd.build import declared_functions as dec
+    diag_names = set(dec([os.path.join(ROOT, "dct_amd", "csrc", "dctq_diag.h")]))
+    assert {"dctq_diag_plan_set_variant", "dctq_diag_movement_planes", "dctq_diag_stream",
+            "dctq_debug_tables"} <= diag_names
+    got = exported(os.path.join(ROOT, "dct_amd", "libdct_amd_diag.so"))
+    assert got == declared_functions() | diag_names, got ^ (declared_functions() | diag_names)
+    assert not (diag_names & exported(os.path.join(ROOT, "dct_amd", "libdct_amd.so")))
+
+
+def test_no_runtime_knobs_in_product():
+    """Kernel selection is not read from the environment: no getenv in the library sources."""
+    csrc = os.path.join(ROOT, "dct_amd", "csrc")
+    for f in os.listdir(csrc):
+        assert "getenv" not in open(os.path.join(csrc, f)).read(), f
 
 
 def test_host_tables_match_reference(lib, blocks):
@@ -62,6 +79,8 @@ def test_host_tables_match_reference(lib, blocks):
 
 
 def test_fastdiv(lib):
+    import dct_amd
+    lib = dct_amd.diag()
     rng = np.random.default_rng(0)
     for d in [1, 2, 3, 7, 60, 240, 480, 32400, 129600, 8294400, 2**31 - 1]:
         for n in list(rng.integers(0, 2**31 - 1, 200)) + [0, d - 1, d, d + 1, 2**31 - 1]:
@@ -125,6 +144,8 @@ def test_constant_block_dc_table(lib):
     resolution in the forward kernel) equals the oracle's reference-order
     forward + quantize of each constant block."""
     import oracle as O
+    import dct_amd
+    lib = dct_amd.diag()
     for q in [1, 10, 25, 50, 75, 90, 100]:
         tab = np.zeros(256, np.int16)
         assert lib.dctq_debug_dc_table(q, tab.ctypes.data) == 0

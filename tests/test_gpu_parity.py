@@ -201,6 +201,105 @@ def test_fallback_counter_and_exactness(T, dm):
     assert ties <= n < ties + 0.05 * by * bx, (n, ties)
 
 
+def _adversarial_row():
+    """One block row of tie-prone blocks: every constant block, two-level checkerboards and stripes."""
+    rng = np.random.default_rng(11)
+    blocks = [np.full((8, 8), v, np.uint8) for v in range(256)]
+    for _ in range(128):
+        a, b = rng.integers(0, 256, 2)
+        m = np.indices((8, 8)).sum(0) % 2 == 0
+        blocks.append(np.where(m, a, b).astype(np.uint8))
+        st = np.zeros((8, 8), np.uint8)
+        st[:, :4], st[:, 4:] = a, b
+        blocks.append(st)
+        blocks.append(st.T.copy())
+    return np.concatenate(blocks, axis=1)
+
+
+@pytest.mark.parametrize("variant", [4, 3, 1])
+def test_forced_kernels_adversarial_and_counter(T, dm, variant):
+    """Small launches normally run v3 (in-place ties), large ones v2 (tie queue,
+    stash, drains): each kernel forced at small sizes through the diagnostic
+    library -- every quality on tie-prone blocks, random planes of
+    every kind, and the fallback counter equal across kernels."""
+    import oracle as O
+    px = _adversarial_row()
+    g = gpu_px(T, px)
+    for q in range(1, 101, 3 if variant == 1 else 1):
+        for ad in (0, 1):
+            got = dm.Plan(q, ad, variant=variant).forward_quant(g).cpu().numpy()
+            assert np.array_equal(got, O.forward_plane(px, q, ad)), (variant, q, ad)
+    for trial in range(8):
+        kind = ["uniform", "smooth", "const", "extreme"][trial % 4]
+        q, ad = [10, 50, 75, 90, 97, 100, 1, 33][trial], trial % 2
+        p = O.synth_plane(700 + trial, O.KINDS[kind], 8 * (17 + 13 * trial), 8 * (5 + 3 * trial))
+        got = dm.Plan(q, ad, variant=variant).forward_quant(gpu_px(T, p)).cpu().numpy()
+        assert np.array_equal(got, O.forward_plane(p, q, ad)), (variant, kind, q, ad)
+    if variant == 1:  # v1 has no constant-block DC table: its exact-path count differs by design
+        return
+    rng = np.random.default_rng(77)
+    sp = gpu_px(T, _step_blocks(rng, 48, 96))
+    counts = []
+    for v in (2, variant):
+        plan = dm.Plan(50, 0, variant=v)
+        cnt = T.zeros(1, dtype=T.int64, device="cuda")
+        plan.set_fallback_counter(cnt)
+        plan.forward_quant(sp)
+        T.cuda.synchronize()
+        counts.append(int(cnt.item()))
+        plan.set_fallback_counter(None)
+    assert counts[0] == counts[1] and counts[0] > 100, counts
+
+
+def test_mid_size_tie_heavy_stream(T, dm):
+    """More than 4096 64-block batches (the product dispatch then runs the v2 queue
+    kernel, not v3) of tie-heavy content: step blocks (a quarter of the DCs are
+    exact ties) and 0/255 extremes, several qualities, both modes."""
+    import oracle as O
+    rng = np.random.default_rng(31)
+    step = _step_blocks(rng, 270, 1024)  # 276 480 blocks = 4320 batches
+    ext = O.synth_plane(5, O.KINDS["extreme"], 8 * 1024, 8 * 270)
+    for px in (step, ext):
+        g = gpu_px(T, px)
+        for q, ad in [(50, 0), (10, 1), (90, 0), (100, 1)]:
+            plan = dm.Plan(q, ad)
+            cnt = T.zeros(1, dtype=T.int64, device="cuda")
+            plan.set_fallback_counter(cnt)
+            got = plan.forward_quant(g).cpu().numpy()
+            plan.set_fallback_counter(None)
+            assert np.array_equal(got, O.forward_plane(px, q, ad, 16)), (q, ad)
+            if q == 50 and px is step:
+                assert int(cnt.item()) > 1000
+
+
+def test_diag_stream_moves_bytes(T, dm):
+    """The hardware-ceiling streams of the diagnostic library (bench.py
+    roofline.movement_ceiling) move what they claim: the flat 1:2 stream writes
+    each 1 KiB input chunk twice (the second copy with bit 0 of its first dword
+    flipped), the write-only stream covers the whole output."""
+    D = dm.diag()
+    n = 64 * 40
+    src = T.randint(0, 256, (n * 64,), dtype=T.uint8, device="cuda")
+    s = T.cuda.current_stream().cuda_stream
+    for kind in (0, 1):
+        dst = T.zeros(n * 128, dtype=T.uint8, device="cuda")
+        assert D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), n, s) == 0
+        T.cuda.synchronize()
+        a = src.view(-1, 4, 1024).cpu().numpy()
+        b = dst.view(-1, 8, 1024).cpu().numpy()
+        assert np.array_equal(b[:, :4], a)
+        flip = b[:, 4:].copy().view(np.uint32)
+        flip.reshape(-1, 4)[:, 0] ^= 1
+        assert np.array_equal(flip.view(np.uint8).reshape(a.shape), a)
+    dst = T.zeros(n * 128, dtype=T.uint8, device="cuda")
+    assert D.dctq_diag_stream(3, src.data_ptr(), dst.data_ptr(), n, s) == 0
+    assert D.dctq_diag_stream(2, src.data_ptr(), dst.data_ptr(), n, s) == 0
+    T.cuda.synchronize()
+    w = dst.view(-1, 16).cpu().numpy().view(np.uint32)
+    assert (w[:, 2] == 7).all() and (w[:, 3] == 9).all()
+    assert D.dctq_diag_stream(9, src.data_ptr(), dst.data_ptr(), n, s) != 0
+
+
 def _step_blocks(rng, by, bx):
     """Left/right two-level blocks: a quarter of their DCs are exact rounding ties at q50."""
     ab = rng.integers(0, 256, (by, bx, 2), dtype=np.uint8)

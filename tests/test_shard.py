@@ -59,6 +59,26 @@ def _worker(rank, world, port, q):
         woff, wsym = O.rle_encode_plane(np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in frames]))
         assert np.array_equal(off.numpy().view(np.uint32), woff), "gathered offsets differ"
         assert np.array_equal(sym.numpy().view(np.uint32), wsym), "gathered symbols differ"
+
+        # (4) bench.py's N>1 gather leg (BASELINE configs[3], strong scaling) end to end:
+        # shard.strong_gather_leg over a ragged frame split, the oracle standing in for the kernel
+        total = 7
+        lo, hi = shard.split(total, world, rank)
+        stack = torch.from_numpy(np.stack([O.synth_plane(300 + f, O.KINDS["uniform"], 32, 24)
+                                           for f in range(total)]))
+        per = (32 // 8) * (24 // 8)
+        counts = [(b - a) * per for a, b in (shard.split(total, world, r) for r in range(world))]
+
+        def forward(fr):
+            return torch.from_numpy(np.concatenate([O.forward_plane(f.numpy(), 75, 0) for f in fr])
+                                    if fr.shape[0] else np.zeros((0, 64), np.int16))
+
+        r = shard.strong_gather_leg(forward, stack[lo:hi], counts, 2, torch.device("cpu"))
+        assert r["blocks_per_step"] == total * per and r["steps"] == 2
+        assert r["kernel_s"] > 0 and r["end_to_end_s"] > 0
+        want = np.concatenate([O.forward_plane(f.numpy(), 75, 0) for f in stack])
+        assert np.array_equal(r["full"].numpy(), want), "strong-scaling gather differs"
+        assert np.array_equal(r["local"].numpy(), want[sum(counts[:rank]):sum(counts[:rank + 1])])
         q.put((rank, "ok"))
     except BaseException as e:  # noqa: BLE001 -- report to the parent
         q.put((rank, repr(e)))

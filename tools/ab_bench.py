@@ -29,8 +29,7 @@ px = dct_amd.synth(7, args.kind, W, H, args.frames)
 nblk = args.frames * (W // 8) * (H // 8)
 plans = {}
 for v in args.variants.split(","):
-    os.environ["DCTQ_FDCT_VARIANT"] = v
-    plans[v] = dct_amd.Plan(args.quality, args.adaptive)
+    plans[v] = dct_amd.Plan(args.quality, args.adaptive, variant=int(v))
 # ONE output buffer shared by the variants (separate buffers put their stores on
 # different physical pages: +-12 % seen on identical code, tools/rle_ab.py)
 out = torch.empty((nblk, 64), dtype=torch.int16, device="cuda")

@@ -15,8 +15,7 @@ nblk = F * (W // 8) * (H // 8)
 px = dct_amd.synth(7, "uniform", W, H, F)
 res = {}
 for var, ad in [(v, a) for a in (0, 1) for v in ("1", "2")]:
-    os.environ["DCTQ_FDCT_VARIANT"] = var
-    plan = dct_amd.Plan(50, ad)
+    plan = dct_amd.Plan(50, ad, variant=int(var))
     vn = torch.empty(nblk, dtype=torch.int32, device="cuda")
     coef = plan.forward_quant(px, var_num=vn)
     ff = torch.empty((nblk, 64), dtype=torch.float32, device="cuda")
@@ -43,7 +42,6 @@ for var, ad in [(v, a) for a in (0, 1) for v in ("1", "2")]:
 
 # ---- zigzag + RLE on the forward-quant output (q50): count+emit and decode
 for kind in ("uniform", "smooth"):
-    os.environ["DCTQ_FDCT_VARIANT"] = "2"
     px2 = dct_amd.synth(9, kind, W, H, F)
     plan = dct_amd.Plan(50, 0)
     coef = plan.forward_quant(px2)

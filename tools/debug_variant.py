@@ -14,8 +14,7 @@ F = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 px = dct_amd.synth(7, "uniform", 3840, 2160, F)
 outs = {}
 for v in (va, vb):
-    os.environ["DCTQ_FDCT_VARIANT"] = v
-    plan = dct_amd.Plan(50, 0)
+    plan = dct_amd.Plan(50, 0, variant=int(v))
     outs[v] = plan.forward_quant(px).cpu().numpy()
 want = O.forward_plane(px[0].cpu().numpy(), 50, 0, 8)
 n0 = want.shape[0]

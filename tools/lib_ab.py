@@ -6,7 +6,7 @@ the first build's (bit-exact builds must agree).
     python tools/lib_ab.py [--rounds 12] [--kind uniform] [--quality 50] [--adaptive 0] LIB...
 
 LIB = path of a .so (tools/ubench/variant.sh / policy.sh output), "default", or
-"movement" (the default build's dctq_diag_movement_planes: the same bytes, no math).
+"movement" (the diagnostic build's dctq_diag_movement_planes: the same bytes, no math).
 """
 import argparse
 import ctypes as C
@@ -43,14 +43,16 @@ stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 builds = {}
 for path in args.libs:
-    p = dct_amd.LIB_PATH if path in ("default", "movement") else os.path.abspath(path)
+    p = {"default": dct_amd.LIB_PATH, "movement": dct_amd.DIAG_PATH}.get(path) or os.path.abspath(path)
     L = C.CDLL(p)
     L.dctq_plan_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.dctq_forward_quant_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p, C.c_void_p,
                                             C.c_void_p]
     h = C.c_void_p()
     assert L.dctq_plan_create(args.quality, args.adaptive, C.byref(h)) == 0
-    L.dctq_diag_movement_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p, C.c_void_p]
+    if path == "movement":
+        L.dctq_diag_movement_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p,
+                                                C.c_void_p]
     builds[os.path.basename(path)] = (L, h)
 
 

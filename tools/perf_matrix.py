@@ -41,7 +41,7 @@ for kind in ("uniform", "smooth", "const", "extreme"):
     y = dct_amd.synth(12345, kind, 3840, 2160, F)
     c = dct_amd.synth(62345, kind, 1920, 1080, 2 * F)
     for q, ad in ((50, 0), (90, 0), (50, 1), (10, 0)):
-        plan = dct_amd.Plan(q, ad)
+        plan = dct_amd.Plan(q, ad, diagnostic=True)
         fb.zero_()
         plan.set_fallback_counter(fb)
         plan.forward_quant_planes([y, c], outs=[oy, oc])

@@ -26,6 +26,7 @@ F = args.frames
 y = dct_amd.synth(1, args.kind, 3840, 2160, F)
 c = dct_amd.synth(2, args.kind, 1920, 1080, 2 * F)
 plan = dct_amd.Plan(args.quality, args.adaptive)
+dplan = dct_amd.Plan(args.quality, args.adaptive, diagnostic=True)  # movement diagnostic (libdct_amd_diag.so)
 ny, nc = F * 480 * 270, 2 * F * 240 * 135
 oy = torch.empty((ny, 64), dtype=torch.int16, device="cuda")
 oc = torch.empty((nc, 64), dtype=torch.int16, device="cuda")
@@ -33,9 +34,9 @@ cases = {
     "luma": (ny, lambda: plan.forward_quant(y, out=oy)),
     "chroma": (nc, lambda: plan.forward_quant(c, out=oc)),
     "luma+chroma (one launch)": (ny + nc, lambda: plan.forward_quant_planes([y, c], outs=[oy, oc])),
-    "movement luma": (ny, lambda: plan.diag_movement_planes([y], [oy])),
-    "movement chroma": (nc, lambda: plan.diag_movement_planes([c], [oc])),
-    "movement luma+chroma": (ny + nc, lambda: plan.diag_movement_planes([y, c], [oy, oc])),
+    "movement luma": (ny, lambda: dplan.diag_movement_planes([y], [oy])),
+    "movement chroma": (nc, lambda: dplan.diag_movement_planes([c], [oc])),
+    "movement luma+chroma": (ny + nc, lambda: dplan.diag_movement_planes([y, c], [oy, oc])),
 }
 for _, fn in cases.values():
     fn()

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
 """HBM traffic per fdct8 launch from two separate rocprofv3 --pmc passes.
 
-    python tools/pmc_traffic.py FETCH_CSV WRITE_CSV --frames F --kind K [-o profiles/traffic.json]
+    python tools/pmc_traffic.py FETCH_CSV WRITE_CSV --frames F --kind K [--quality Q --adaptive A]
+                                [-o profiles/traffic.json]
+
+The record carries the configuration and the sha256 of dct_amd/libdct_amd.so:
+bench.py uses it only for a run with the same frames, kind, quality, adaptive
+mode, launches per step and library build.
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reports half of the
 bytes of a coalesced streaming read (MI355X_MICROARCH.md "HBM"), so the read
@@ -12,8 +17,12 @@ averaged over every forward-quant dispatch the same way.
 """
 import argparse
 import csv
+import hashlib
 import json
+import os
 import statistics
+
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dct_amd", "libdct_amd.so")
 
 
 def per_dispatch(path, counter, match):
@@ -30,6 +39,8 @@ def main():
     ap.add_argument("write")
     ap.add_argument("--frames", type=int, required=True)
     ap.add_argument("--kind", required=True)
+    ap.add_argument("--quality", type=int, default=50)
+    ap.add_argument("--adaptive", type=int, default=0)
     ap.add_argument("--kernel", default="fdct8_quant_v2")
     ap.add_argument("--launches", type=int, default=1, help="forward-quant dispatches per bench step")
     ap.add_argument("-o", "--out", default="profiles/traffic.json")
@@ -41,7 +52,8 @@ def main():
     rd = 2 * statistics.mean(f) * 1024
     wr = statistics.mean(w) * 1024
     blocks = a.frames * (480 * 270 + 2 * 240 * 135) / a.launches  # average blocks per launch
-    out = {"kernel": a.kernel, "frames": a.frames, "kind": a.kind, "dispatches": len(f),
+    out = {"kernel": a.kernel, "frames": a.frames, "kind": a.kind, "quality": a.quality, "adaptive": a.adaptive,
+           "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(), "dispatches": len(f),
            "launches_per_step": a.launches,
            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
            "algorithmic_bytes_per_launch": 192 * blocks, "traffic_over_algorithmic": (rd + wr) / (192 * blocks),

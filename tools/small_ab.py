@@ -1,5 +1,5 @@
 """Single-frame launches (BASELINE configs[1] 512x512, one 4K 4:2:0 frame) with
-the queue kernel forced (DCTQ_FDCT_VARIANT=4) against the default dispatch
+the queue kernel forced (Plan(variant=4), diagnostic library) against the default dispatch
 (variant 2: in-place ties when every wave has at most one batch), same inputs,
 back-to-back launches timed with HIP events, outputs compared.
 
@@ -16,8 +16,7 @@ import dct_amd  # noqa: E402
 
 plans = {}
 for v in ("4", "2"):
-    os.environ["DCTQ_FDCT_VARIANT"] = v
-    plans[v] = dct_amd.Plan(50, 0)
+    plans[v] = dct_amd.Plan(50, 0, variant=int(v))
 cases = {"512x512": [dct_amd.synth(3, "uniform", 512, 512)],
          "4K 4:2:0 frame": [dct_amd.synth(4, "uniform", 3840, 2160), dct_amd.synth(5, "uniform", 1920, 1080, 2)]}
 for name, planes in cases.items():
