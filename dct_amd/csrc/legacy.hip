@@ -2,11 +2,10 @@
 // include/quantization.h, include/utils.h) as a drop-in, backed by the GPU.
 //
 // Each call marshals its row-pointer arrays into one pinned, device-mapped
-// staging buffer, runs a small exact kernel that reads it over the host link,
-// repeats the reference's fp64 arithmetic in the same order (this file is
-// compiled with -ffp-contract=off) and writes the result back into it --
-// bit-identical to src/dct.c and src/quantization.c for any block size
-// up to 64.  It is a drop-in for callers that stay per-block; frame-level
+// staging buffer (or, for large blocks, a device scratch buffer), runs a small
+// exact kernel, repeats the reference's fp64 arithmetic in the same order (this
+// file is compiled with -ffp-contract=off) and copies the result back --
+// bit-identical to src/dct.c and src/quantization.c for any block size.  It is a drop-in for callers that stay per-block; frame-level
 // callers should use include/dct_amd.h (one launch per plane).
 //
 // Conventions kept from the reference: no return codes; failures print to
@@ -41,49 +40,50 @@ namespace {
         if (e_ != hipSuccess) die(what, e_);      \
     } while (0)
 
-constexpr int kMaxN = 64;
-
 // ---------------------------------------------------------------- kernels
-// src/dct.c:52-77 (forward) and :80-105 (inverse) -- one workgroup per block.
-// `d` and `in` live in pinned host memory (zero-copy staging, see Staging): the
-// workgroup first copies them into LDS in one parallel round trip over the host
-// link (d stays in host memory when 3 n^2 doubles exceed kLdsTables), then runs
-// both passes from LDS and writes `out` straight back to host memory.
-constexpr int kLdsTables = 48 * 1024;
-__device__ __forceinline__ const double *stage_in(const double *__restrict__ src, double *dst, int nn) {
-    for (int e = threadIdx.x; e < nn; e += blockDim.x) dst[e] = src[e];
-    return dst;
+// src/dct.c:52-77 (forward) and :80-105 (inverse).  Both passes of both
+// transforms are Z[i][j] = ((0 + X[i][0] Y[0][j]) + X[i][1] Y[1][j]) + ...:
+//   forward: temp = input * T (T = ctx->transposed_dct, :61), out = D * temp (:72)
+//   inverse: temp = T * input (:89),                    out = temp * D (:100)
+// with D = ctx->dct_matrix -- the two PUBLIC tables exactly as the caller holds
+// them (a caller may have edited either).  Separate multiply and add (this file
+// is compiled with -ffp-contract=off), k ascending, accumulators from +0.0.
+__device__ __forceinline__ double dot_ordered(const double *x, const double *y, int n, int i, int j) {
+    double acc = 0.0;
+    for (int k = 0; k < n; ++k) acc += x[i * n + k] * y[k * n + j];
+    return acc;
 }
 
+// Small blocks (4 n^2 doubles <= kLdsBytes: n <= 32, the codec's n = 8): ONE
+// workgroup per call, its D, T and input staged in LDS from the pinned zero-copy
+// buffer in one parallel round trip over the host link, the result written
+// straight back to it.
+constexpr int kLdsBytes = 32 * 1024;
 template <bool FWD>
-__global__ void k_transform(int n, const double *__restrict__ dh, const double *__restrict__ inh,
-                            double *__restrict__ out) {
+__global__ void k_transform_small(int n, const double *__restrict__ dh, const double *__restrict__ th,
+                                  const double *__restrict__ inh, double *__restrict__ out) {
     extern __shared__ double lds[];
     const int nn = n * n;
-    const bool dl = 3 * nn * (int)sizeof(double) <= kLdsTables;
-    double *tmp = lds, *in = lds + nn;
-    const double *d = dl ? stage_in(dh, lds + 2 * nn, nn) : dh;
-    stage_in(inh, in, nn);
-    __syncthreads();
+    double *d = lds, *t = lds + nn, *in = lds + 2 * nn, *tmp = lds + 3 * nn;
     for (int e = threadIdx.x; e < nn; e += blockDim.x) {
-        const int i = e / n, j = e % n;
-        double acc = 0.0;
-        if (FWD)
-            for (int k = 0; k < n; ++k) acc += in[i * n + k] * d[j * n + k];  // input[i][k] * D^T[k][j]
-        else
-            for (int k = 0; k < n; ++k) acc += d[k * n + i] * in[k * n + j];  // D^T[i][k] * input[k][j]
-        tmp[e] = acc;
+        d[e] = dh[e];
+        t[e] = th[e];
+        in[e] = inh[e];
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < nn; e += blockDim.x) {
-        const int i = e / n, j = e % n;
-        double acc = 0.0;
-        if (FWD)
-            for (int k = 0; k < n; ++k) acc += d[i * n + k] * tmp[k * n + j];
-        else
-            for (int k = 0; k < n; ++k) acc += tmp[i * n + k] * d[k * n + j];
-        out[e] = acc;
-    }
+    for (int e = threadIdx.x; e < nn; e += blockDim.x)
+        tmp[e] = FWD ? dot_ordered(in, t, n, e / n, e % n) : dot_ordered(t, in, n, e / n, e % n);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nn; e += blockDim.x)
+        out[e] = FWD ? dot_ordered(d, tmp, n, e / n, e % n) : dot_ordered(tmp, d, n, e / n, e % n);
+}
+
+// Any n (the reference takes any block size, src/dct.c:7-40): the packed
+// tables and input are copied to device memory once, each pass is its own
+// launch over all n^2 elements, one element per thread.
+__global__ void k_pass(int n, const double *__restrict__ x, const double *__restrict__ y, double *__restrict__ z) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < (long long)n * n) z[e] = dot_ordered(x, y, n, (int)(e / n), (int)(e % n));
 }
 
 // src/quantization.c:171-211 element (i,j) of the adjusted matrix.
@@ -122,10 +122,12 @@ __global__ void k_elementwise(int mode, int nn, const double *__restrict__ m, in
 }
 
 // src/quantization.c:153-169 -- sequential row-major sums (order matters for
-// non-integer input), after one parallel copy of the block into LDS.
-__global__ void k_variance(int nn, const double *__restrict__ xh, double *__restrict__ out) {
+// non-integer input), one thread; small blocks first copied from the zero-copy
+// buffer into LDS by the whole workgroup (one parallel round trip over the
+// host link), large ones read from device scratch.
+__global__ void k_variance_small(int nn, const double *__restrict__ xh, double *__restrict__ out) {
     extern __shared__ double x[];
-    stage_in(xh, x, nn);
+    for (int e = threadIdx.x; e < nn; e += blockDim.x) x[e] = xh[e];
     __syncthreads();
     if (threadIdx.x != 0) return;
     double s = 0.0, s2 = 0.0;
@@ -137,11 +139,25 @@ __global__ void k_variance(int nn, const double *__restrict__ xh, double *__rest
     out[0] = (s2 / nn) - (mean * mean);
 }
 
+__global__ void k_variance(int nn, const double *__restrict__ x, double *__restrict__ out) {
+    double s = 0.0, s2 = 0.0;
+    for (int k = 0; k < nn; ++k) {
+        s += x[k];
+        s2 += x[k] * x[k];
+    }
+    const double mean = s / nn;
+    out[0] = (s2 / nn) - (mean * mean);
+}
+
 // ---------------------------------------------------------------- staging
-// Zero-copy: one pinned, device-mapped host buffer per thread.  A call packs its
-// row-pointer arrays into it, launches one kernel that reads its inputs from it
-// and writes its outputs back into it over the host link, and synchronizes: no
-// memcpy calls (each was a synchronous round trip through the driver).
+// Zero-copy: one pinned, device-mapped host buffer.  A call packs its row-pointer
+// arrays into it, launches a kernel that reads its inputs from it and writes its
+// outputs back into it over the host link, and synchronizes: no memcpy calls.
+// Larger blocks go through a device scratch buffer instead (copied once each
+// way).  One buffer of each for the process: every entry point holds the
+// library-wide entry lock (DCTQ_ENTRY), so calls never overlap, and a thread
+// that exits leaves nothing behind.  Both are grown on demand and kept for the
+// life of the process (their memory goes back with it).
 struct Staging {
     unsigned char *host = nullptr;  // pinned host memory
     unsigned char *dev = nullptr;   // the same pages as seen by the device
@@ -157,7 +173,21 @@ struct Staging {
         return host;
     }
 };
-thread_local Staging g_stage;
+struct Scratch {
+    unsigned char *dev = nullptr;
+    size_t bytes = 0;
+    unsigned char *get(size_t need) {
+        if (need > bytes) {
+            if (dev) (void)hipFree(dev);
+            dev = nullptr;
+            LCHK(hipMalloc((void **)&dev, need), "hipMalloc(legacy scratch)");
+            bytes = need;
+        }
+        return dev;
+    }
+};
+Staging g_stage;
+Scratch g_scratch;
 
 void finish(const char *what) {
     LCHK(hipGetLastError(), what);
@@ -165,32 +195,58 @@ void finish(const char *what) {
 }
 
 void pack(double **a, int n, double *dst) {
-    for (int i = 0; i < n; ++i) memcpy(dst + i * n, a[i], sizeof(double) * n);
+    for (int i = 0; i < n; ++i) memcpy(dst + (size_t)i * n, a[i], sizeof(double) * n);
 }
 void unpack(const double *src, int n, double **a) {
-    for (int i = 0; i < n; ++i) memcpy(a[i], src + i * n, sizeof(double) * n);
+    for (int i = 0; i < n; ++i) memcpy(a[i], src + (size_t)i * n, sizeof(double) * n);
 }
 
 void check_n(int n) {
-    if (n < 1 || n > kMaxN) die("block_size out of the supported range 1..64");
+    if (n < 1 || n > 46340) die("block_size out of the supported range 1..46340");  // n^2 fits an int
 }
 
 void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
     DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
-    const int n = ctx->block_size, nn = n * n;
+    const int n = ctx->block_size;
     check_n(n);
-    double *h = (double *)g_stage.get(sizeof(double) * 3 * nn);
-    const double *dv = (const double *)g_stage.dev;
-    pack(ctx->dct_matrix, n, h);
-    pack(input, n, h + nn);
-    const int threads = nn < 256 ? ((nn + 63) / 64) * 64 : 256;
-    const size_t lds = sizeof(double) * (3 * nn * sizeof(double) <= (size_t)kLdsTables ? 3 * nn : 2 * nn);
-    if (fwd)
-        hipLaunchKernelGGL(k_transform<true>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, (double *)dv + 2 * nn);
-    else
-        hipLaunchKernelGGL(k_transform<false>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, (double *)dv + 2 * nn);
-    finish("transform launch");
-    unpack(h + 2 * nn, n, output);
+    const size_t nn = (size_t)n * n;
+    if (4 * nn * sizeof(double) <= (size_t)kLdsBytes) {
+        double *h = (double *)g_stage.get(sizeof(double) * 4 * nn);
+        const double *dv = (const double *)g_stage.dev;
+        pack(ctx->dct_matrix, n, h);
+        pack(ctx->transposed_dct, n, h + nn);
+        pack(input, n, h + 2 * nn);
+        const int threads = nn < 256 ? (int)((nn + 63) / 64) * 64 : 256;
+        const size_t lds = sizeof(double) * 4 * nn;
+        if (fwd)
+            hipLaunchKernelGGL(k_transform_small<true>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, dv + 2 * nn,
+                               (double *)dv + 3 * nn);
+        else
+            hipLaunchKernelGGL(k_transform_small<false>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, dv + 2 * nn,
+                               (double *)dv + 3 * nn);
+        finish("transform launch");
+        unpack(h + 3 * nn, n, output);
+        return;
+    }
+    // any n: D | T | input | temp | output in device scratch
+    std::vector<double> h(3 * nn);
+    pack(ctx->dct_matrix, n, h.data());
+    pack(ctx->transposed_dct, n, h.data() + nn);
+    pack(input, n, h.data() + 2 * nn);
+    double *d = (double *)g_scratch.get(sizeof(double) * 5 * nn), *t = d + nn, *in = d + 2 * nn, *tmp = d + 3 * nn,
+           *out = d + 4 * nn;
+    LCHK(hipMemcpy(d, h.data(), sizeof(double) * 3 * nn, hipMemcpyHostToDevice), "hipMemcpy(legacy transform in)");
+    const unsigned grid = (unsigned)((nn + 255) / 256);
+    if (fwd) {
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, in, t, tmp);
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, d, tmp, out);
+    } else {
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, t, in, tmp);
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, tmp, d, out);
+    }
+    LCHK(hipGetLastError(), "transform launch");
+    LCHK(hipMemcpy(h.data(), out, sizeof(double) * nn, hipMemcpyDeviceToHost), "hipMemcpy(legacy transform out)");
+    unpack(h.data(), n, output);
 }
 
 // One elementwise launch over an n x n block; inputs/outputs as flat host arrays.
@@ -198,7 +254,7 @@ void elementwise(int mode, int n, double **m, int flag, double variance, const d
                  double *dout, int *iout) {
     DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int nn = n * n;
-    const size_t bytes = sizeof(double) * 3 * nn + sizeof(int) * 2 * nn;
+    const size_t bytes = sizeof(double) * 3 * (size_t)nn + sizeof(int) * 2 * (size_t)nn;
     unsigned char *h = g_stage.get(bytes);
     double *hm = (double *)h, *hd = hm + nn;
     int *hi = (int *)(hd + 2 * nn);
@@ -359,14 +415,25 @@ void dequantize(QuantContext *ctx, int **quant_coeffs, double **dct_coeffs, doub
 double calculate_block_variance(double **block, int block_size) {
     DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     check_n(block_size);
-    const int nn = block_size * block_size;
-    double *h = (double *)g_stage.get(sizeof(double) * (nn + 1));
-    double *dv = (double *)g_stage.dev;
-    pack(block, block_size, h);
-    const int threads = nn < 256 ? ((nn + 63) / 64) * 64 : 256;
-    hipLaunchKernelGGL(k_variance, dim3(1), dim3(threads), sizeof(double) * nn, 0, nn, dv, dv + nn);
-    finish("variance launch");
-    return h[nn];
+    const size_t nn = (size_t)block_size * block_size;
+    if (nn * sizeof(double) <= (size_t)kLdsBytes) {
+        double *hs = (double *)g_stage.get(sizeof(double) * (nn + 1));
+        double *dv = (double *)g_stage.dev;
+        pack(block, block_size, hs);
+        const int threads = nn < 256 ? (int)((nn + 63) / 64) * 64 : 256;
+        hipLaunchKernelGGL(k_variance_small, dim3(1), dim3(threads), sizeof(double) * nn, 0, (int)nn, dv, dv + nn);
+        finish("variance launch");
+        return hs[nn];
+    }
+    std::vector<double> h(nn);
+    pack(block, block_size, h.data());
+    double *dv = (double *)g_scratch.get(sizeof(double) * (nn + 1));
+    LCHK(hipMemcpy(dv, h.data(), sizeof(double) * nn, hipMemcpyHostToDevice), "hipMemcpy(variance in)");
+    hipLaunchKernelGGL(k_variance, dim3(1), dim3(1), 0, 0, (int)nn, dv, dv + nn);
+    LCHK(hipGetLastError(), "variance launch");
+    double v;
+    LCHK(hipMemcpy(&v, dv + nn, sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy(variance out)");
+    return v;
 }
 
 double **adjust_matrix_for_block(QuantContext *ctx, double variance, int is_quantize) {

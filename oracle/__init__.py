@@ -49,6 +49,8 @@ def _load_orc():
     lib.orc_clamp_quality.restype = C.c_int
     lib.orc_forward.argtypes = [C.c_int, _dp, _dp, _dp]
     lib.orc_inverse.argtypes = [C.c_int, _dp, _dp, _dp]
+    lib.orc_forward_tables.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
+    lib.orc_inverse_tables.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
     lib.orc_variance.argtypes = [C.c_int, _dp]
     lib.orc_variance.restype = C.c_double
     lib.orc_adjust.argtypes = [C.c_int, _dp, C.c_double, C.c_int, _dp]
@@ -101,6 +103,8 @@ def ref(build: str = "O2"):
         lib.ref_quant_tables.argtypes = [C.c_int, C.c_int, C.c_int, _dp, _dp, C.POINTER(C.c_int)]
         lib.ref_forward.argtypes = [C.c_int, _dp, _dp]
         lib.ref_inverse.argtypes = [C.c_int, _dp, _dp]
+        lib.ref_forward_tables.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
+        lib.ref_inverse_tables.argtypes = [C.c_int, _dp, _dp, _dp, _dp]
         lib.ref_variance.argtypes = [C.c_int, _dp]
         lib.ref_variance.restype = C.c_double
         lib.ref_quantize.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, _dp, _ip]
@@ -149,6 +153,25 @@ def inverse(c: np.ndarray) -> np.ndarray:
     n = c.shape[0]
     out = np.zeros(n * n)
     orc().orc_inverse(n, dct_matrix(n).ravel(), np.ascontiguousarray(c, np.float64).ravel(), out)
+    return out.reshape(n, n)
+
+
+def forward_tables(x: np.ndarray, d: np.ndarray, t: np.ndarray) -> np.ndarray:
+    """dct_forward on a context whose public tables are d (dct_matrix) and t
+    (transposed_dct) as given -- src/dct.c:52-77 reads t in its first pass."""
+    n = x.shape[0]
+    out = np.zeros(n * n)
+    orc().orc_forward_tables(n, np.ascontiguousarray(d, np.float64).ravel(), np.ascontiguousarray(t, np.float64).ravel(),
+                             np.ascontiguousarray(x, np.float64).ravel(), out)
+    return out.reshape(n, n)
+
+
+def inverse_tables(c: np.ndarray, d: np.ndarray, t: np.ndarray) -> np.ndarray:
+    """dct_inverse with the public tables as given (src/dct.c:80-105)."""
+    n = c.shape[0]
+    out = np.zeros(n * n)
+    orc().orc_inverse_tables(n, np.ascontiguousarray(d, np.float64).ravel(), np.ascontiguousarray(t, np.float64).ravel(),
+                             np.ascontiguousarray(c, np.float64).ravel(), out)
     return out.reshape(n, n)
 
 

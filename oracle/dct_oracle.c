@@ -78,39 +78,79 @@ int orc_clamp_quality(int quality) {
     return quality;
 }
 
-/* src/dct.c:52-77: temp = X * D^T (k ascending), out = D * temp (k ascending),
- * each accumulator starting at 0.0, separate multiply and add. */
-void orc_forward(int n, const double *d, const double *x, double *out) {
-    double tmp[64 * 64];
+/* src/dct.c:52-77 with the context's two public tables as given: temp = X * T
+ * (T = ctx->transposed_dct, :61), out = D * temp (D = ctx->dct_matrix, :72),
+ * k ascending, each accumulator starting at 0.0, separate multiply and add;
+ * any n (temp on the heap, as the reference allocates it, :54). */
+static void orc_forward_core(int n, const double *d, const double *t, const double *x, double *out, double *tmp) {
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j) {
             double acc = 0.0;
-            for (int k = 0; k < n; ++k) acc += x[i * n + k] * d[j * n + k]; /* D^T[k][j] = D[j][k] */
-            tmp[i * n + j] = acc;
+            for (int k = 0; k < n; ++k) acc += x[(size_t)i * n + k] * t[(size_t)k * n + j];
+            tmp[(size_t)i * n + j] = acc;
         }
     for (int i = 0; i < n; ++i)
         for (int j = 0; j < n; ++j) {
             double acc = 0.0;
-            for (int k = 0; k < n; ++k) acc += d[i * n + k] * tmp[k * n + j];
-            out[i * n + j] = acc;
+            for (int k = 0; k < n; ++k) acc += d[(size_t)i * n + k] * tmp[(size_t)k * n + j];
+            out[(size_t)i * n + j] = acc;
         }
 }
 
-/* src/dct.c:80-105: temp = D^T * C, out = temp * D. */
+void orc_forward_tables(int n, const double *d, const double *t, const double *x, double *out) {
+    double *tmp = malloc(sizeof(double) * (size_t)n * n);
+    if (!tmp) abort();
+    orc_forward_core(n, d, t, x, out, tmp);
+    free(tmp);
+}
+
+/* src/dct.c:80-105 with the public tables as given: temp = T * C (:89),
+ * out = temp * D (:100). */
+void orc_inverse_tables(int n, const double *d, const double *t, const double *c, double *out) {
+    double *tmp = malloc(sizeof(double) * (size_t)n * n);
+    if (!tmp) abort();
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) acc += t[(size_t)i * n + k] * c[(size_t)k * n + j];
+            tmp[(size_t)i * n + j] = acc;
+        }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k) acc += tmp[(size_t)i * n + k] * d[(size_t)k * n + j];
+            out[(size_t)i * n + j] = acc;
+        }
+    free(tmp);
+}
+
+static double *orc_transposed(int n, const double *d) {
+    double *t = malloc(sizeof(double) * (size_t)n * n);
+    if (!t) abort();
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) t[(size_t)i * n + j] = d[(size_t)j * n + i]; /* src/dct.c:33-37 */
+    return t;
+}
+
+/* The context dct_init builds: T = D^T exactly (src/dct.c:33-37). */
+void orc_forward(int n, const double *d, const double *x, double *out) {
+    double *t = orc_transposed(n, d);
+    orc_forward_tables(n, d, t, x, out);
+    free(t);
+}
+
+/* 8x8 forward for the plane loops: T and temp on the stack. */
+static void orc_forward8(const double *d, const double *x, double *out) {
+    double t[64], tmp[64];
+    for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) t[i * 8 + j] = d[j * 8 + i];
+    orc_forward_core(8, d, t, x, out, tmp);
+}
+
 void orc_inverse(int n, const double *d, const double *c, double *out) {
-    double tmp[64 * 64];
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) {
-            double acc = 0.0;
-            for (int k = 0; k < n; ++k) acc += d[k * n + i] * c[k * n + j]; /* D^T[i][k] = D[k][i] */
-            tmp[i * n + j] = acc;
-        }
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) {
-            double acc = 0.0;
-            for (int k = 0; k < n; ++k) acc += tmp[i * n + k] * d[k * n + j];
-            out[i * n + j] = acc;
-        }
+    double *t = orc_transposed(n, d);
+    orc_inverse_tables(n, d, t, c, out);
+    free(t);
 }
 
 /* src/quantization.c:153-169: row-major sum / sum of squares, mean = sum/count,
@@ -197,7 +237,7 @@ static void orc_rows(orc_job *jb) {
         for (int bx = 0; bx < jb->bw; ++bx) {
             long b = (long)by * jb->bw + bx;
             orc_block_from_pixels(jb->px, jb->stride, by * 8, bx * 8, 8, x);
-            orc_forward(8, jb->d, x, c);
+            orc_forward8(jb->d, x, c);
             if (jb->fout) memcpy(jb->fout + b * 64, c, sizeof c);
             if (jb->out) {
                 double var = jb->adaptive ? orc_variance(8, x) : 0.0;

@@ -8,6 +8,9 @@ void orc_quant_matrix(int n, int quality, double *q);
 void orc_dequant_matrix(int n, const double *q, double *dq);
 int orc_clamp_quality(int quality);
 void orc_forward(int n, const double *d, const double *x, double *out);
+/* the same with the context's public tables as given (D = dct_matrix, T = transposed_dct) */
+void orc_forward_tables(int n, const double *d, const double *t, const double *x, double *out);
+void orc_inverse_tables(int n, const double *d, const double *t, const double *c, double *out);
 void orc_inverse(int n, const double *d, const double *c, double *out);
 double orc_variance(int n, const double *x);
 void orc_adjust(int n, const double *src, double variance, int is_quantize, double *m);

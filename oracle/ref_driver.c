@@ -61,6 +61,32 @@ void ref_inverse(int n, const double *x, double *out) {
     dct_free(c);
 }
 
+/* dct_forward / dct_inverse on a context whose PUBLIC tables the caller set:
+ * dct_init(n), then ctx->dct_matrix := d and ctx->transposed_dct := t. */
+static void ref_tables_call(int n, const double *d, const double *t, const double *x, double *out, int fwd) {
+    DCTContext *c = dct_init(n);
+    to2d(d, c->dct_matrix, n);
+    to2d(t, c->transposed_dct, n);
+    double **a = alloc_array(n, n), **b = alloc_array(n, n);
+    to2d(x, a, n);
+    if (fwd)
+        dct_forward(c, a, b);
+    else
+        dct_inverse(c, a, b);
+    from2d(b, out, n);
+    free_array(a, n);
+    free_array(b, n);
+    dct_free(c);
+}
+
+void ref_forward_tables(int n, const double *d, const double *t, const double *x, double *out) {
+    ref_tables_call(n, d, t, x, out, 1);
+}
+
+void ref_inverse_tables(int n, const double *d, const double *t, const double *x, double *out) {
+    ref_tables_call(n, d, t, x, out, 0);
+}
+
 double ref_variance(int n, const double *x) {
     double **a = alloc_array(n, n);
     to2d(x, a, n);

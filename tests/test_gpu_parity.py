@@ -598,12 +598,13 @@ def test_legacy_transforms_bit_exact(L, blocks):
 
 
 def test_legacy_large_blocks_and_variance(L):
-    """The per-block API at the sizes where the legacy kernels change staging (3 n^2 doubles above 48 KiB:
-    the DCT table is read from pinned host memory instead of LDS) up to the maximum n = 64, against the
-    oracle's restatement (bit-exact doubles); the variance of the same blocks (reference order)."""
+    """The per-block API on both sides of the legacy kernels' staging switch (4 n^2 doubles up to 32 KiB:
+    one workgroup with D, T and the block in LDS over the zero-copy buffer; above: device scratch and one
+    launch per pass), against the oracle's restatement (bit-exact doubles); the variance of the same blocks
+    (reference order)."""
     import oracle as O
     rng = np.random.default_rng(77)
-    for n in (32, 44, 45, 64):
+    for n in (31, 32, 33, 45, 64, 65):
         ctx = L.dct_init(n)
         x = rng.integers(-128, 128, (n, n)).astype(np.float64) + rng.random((n, n))
         a, b, c = _put(L, x), L.alloc_array(n, n), L.alloc_array(n, n)
@@ -614,6 +615,50 @@ def test_legacy_large_blocks_and_variance(L):
         v = L.calculate_block_variance(a, n)
         assert np.float64(v).view(np.uint64) == np.float64(O.variance(x)).view(np.uint64), n
         for m in (a, b, c):
+            L.free_array(m, n)
+        L.dct_free(ctx)
+
+
+def _set_table(m, a):
+    n = a.shape[0]
+    for i in range(n):
+        for j in range(n):
+            m[i][j] = float(a[i, j])
+
+
+def test_legacy_public_tables_and_large_n(L):
+    """dct_forward / dct_inverse read the context's PUBLIC tables
+    as the caller holds them (transposed_dct in the first pass, src/dct.c:61,89;
+    dct_matrix in the second), for any block size the reference accepts (dct_init
+    takes any n, src/dct.c:7-40) -- bit-exact against digests of the compiled
+    reference's own outputs (tests/golden/legacy_tables.json); the variance of the
+    large blocks against the oracle."""
+    import hashlib
+    import json
+    import sys
+    import oracle as O
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_legacy_golden import case_inputs
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "legacy_tables.json")))
+    for c in g["cases"]:
+        n = c["n"]
+        x, d, t = case_inputs(n, c["seed"], c["edit"])
+        ctx = L.dct_init(n)
+        if c["edit"] is None:
+            assert (_get(ctx.contents.dct_matrix, n).view(np.uint64) == d.view(np.uint64)).all(), c["name"]
+        else:
+            _set_table(ctx.contents.dct_matrix, d)
+            _set_table(ctx.contents.transposed_dct, t)
+        a, b, e = _put(L, x), L.alloc_array(n, n), L.alloc_array(n, n)
+        L.dct_forward(ctx, a, b)
+        fw = _get(b, n)
+        assert hashlib.sha256(fw.tobytes()).hexdigest() == c["forward_sha256"], c["name"]
+        L.dct_inverse(ctx, b, e)
+        assert hashlib.sha256(_get(e, n).tobytes()).hexdigest() == c["inverse_of_forward_sha256"], c["name"]
+        if c["edit"] is None and n > 64:
+            v = L.calculate_block_variance(a, n)
+            assert np.float64(v).view(np.uint64) == np.float64(O.variance(x)).view(np.uint64), n
+        for m in (a, b, e):
             L.free_array(m, n)
         L.dct_free(ctx)
 

@@ -5,12 +5,14 @@ The fixtures in tests/golden/ were produced by the reference itself
 clean-room restatement reproduces them bit for bit, so the GPU tests can use it
 as the checker at sizes the fixtures do not cover."""
 import hashlib
+import json
+import os
 
 import numpy as np
 import pytest
 
 import oracle as O
-from conftest import f64
+from conftest import ROOT, f64
 
 QUALITIES = [1, 10, 25, 50, 75, 90, 100]
 
@@ -233,3 +235,22 @@ def test_huffman_bucket_model_is_exact():
         amp = int(rng.choice([1, 2, 3, 8, 100, 1024]))
         blk = rng.integers(-amp, amp + 1, 64) * (rng.random(64) < dens)
         assert bucket_merge_bits(blk) == O.huffman_bits(blk), blk.tolist()
+
+
+def test_legacy_tables_golden():
+    """The oracle's explicit-table transforms reproduce the reference's outputs for
+    block sizes above 64 and for caller-edited public tables (tests/golden/
+    make_legacy_golden.py, generated from the compiled reference)."""
+    import hashlib
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from make_legacy_golden import case_inputs
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "legacy_tables.json")))
+    for c in g["cases"]:
+        x, d, t = case_inputs(c["n"], c["seed"], c["edit"])
+        fw = O.forward_tables(x, d, t)
+        assert hashlib.sha256(fw.tobytes()).hexdigest() == c["forward_sha256"], c["name"]
+        inv = O.inverse_tables(fw, d, t)
+        assert hashlib.sha256(inv.tobytes()).hexdigest() == c["inverse_of_forward_sha256"], c["name"]
+        if c["edit"] is None:
+            assert np.array_equal(O.forward(x).view(np.uint64), fw.view(np.uint64))
