@@ -34,8 +34,9 @@
 // at most 16 / 32 nonzero coefficients (natural content), just those, compacted
 // through LDS -- adds one count per run length into its column of an LDS
 // histogram (16-bit counters, two lanes per dword, ds_add_u32), then runs the
-// bucket merge.  Dense tiles whose every block's values span < 64 integers
-// (q50 noise, most natural content) skip the sort: dense_counts below.  VALU-bound (~2000 instructions per 64 dense blocks).
+// bucket merge.  Tiles whose every block's values span < 64 integers (q50
+// noise, most natural content) skip the sort: narrow_counts below.  VALU-bound
+// (DESIGN.md 3.8).
 // DCTQ_HUF_MIN_WAVES (launch bound, default 3 waves/SIMD: 168 VGPRs) is an A/B knob.
 #include "dctq_internal.h"
 
@@ -44,7 +45,14 @@ namespace dctq {
 constexpr int kHufWaves = 4;
 constexpr int kHufThreads = 64 * kHufWaves;
 constexpr int kHufPitch = 144;  // bytes per block in the tile stage (128 + 16: ds_read_b128 spread)
-constexpr int kHufWaveLds = 12288;  // >= 64 * kHufPitch and 8 KiB histogram + 4 KiB counters
+constexpr int kHufWaveLds = 64 * kHufPitch;  // the tile stage, reused for the histogram (kHistBytes)
+// The narrow path's value counters and weight histogram, one region shared by
+// the workgroup's waves: byte  row * 256 + lane * 4 + wave  is wave `wave`'s
+// 8-bit counter `row` of lane `lane` (counts never exceed 64).  Every lane owns
+// a dword per row (conflict-free banks), the wave owns a byte of it (its adds
+// are 1 << 8 * wave), and one v_perm builds a dword address from a value (byte
+// 1 = the row, byte 0 = lane * 4).  Rows 0..63: value vmin + row; then rows 0..64: leaf / node weight.
+constexpr int kHufCtrBytes = 65 * 256;
 
 __device__ __forceinline__ void cas(uint32_t &a, uint32_t &b) {
     const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
@@ -67,12 +75,21 @@ __device__ __forceinline__ void sort_net(uint32_t (&a)[N]) {
                     if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cas(a[i + j], a[i + j + k]);
 }
 
-// Histogram column of `lane`: 16-bit counter of weight w (1..64) at byte
-// (w-1)*128 + lane*2 (dword (w-1)*32 + lane/2: lanes 2q, 2q+1 share a dword,
-// bank q -- conflict-free for any mix of weights across lanes).
+// Histogram column of `lane`: 16-bit counter of weight w (0..64) at byte
+// w*128 + lane*2 (dword w*32 + lane/2: lanes 2q, 2q+1 share a dword, bank q --
+// conflict-free for any mix of weights across lanes).  Bucket 0 is a dummy that
+// absorbs "no leaf" adds, so the count loops stay branch-free.  65 buckets =
+// 8 320 B, inside the wave's 9 KiB tile stage.
+constexpr int kHistBytes = 65 * 128;
 __device__ __forceinline__ void hist_add(char *h, int w, int lane, uint32_t n) {
-    __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(h + (w - 1) * 128 + (lane & ~1) * 2), n << (16 * (lane & 1)),
+    __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(h + w * 128 + (lane & ~1) * 2), n << (16 * (lane & 1)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+// zero the wave's histogram (9 KiB: buckets 0..64)
+__device__ __forceinline__ void hist_zero(char *mine, int lane) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
 }
 
 // Occupancy of the lane's histogram: bit w-1 set while bucket w may hold nodes
@@ -152,8 +169,7 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
     sort_net<N>(b);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): column reads done before the histogram overwrites them
     __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
+    hist_zero(mine, lane);
     __builtin_amdgcn_wave_barrier();
     runs_to_hist<N, false>(b, mine, lane, nodes, lmax);
 }
@@ -173,50 +189,94 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
     sort_net<64>(a);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile reads are done before the histogram overwrites them
     __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
+    hist_zero(mine, lane);
     __builtin_amdgcn_wave_barrier();
     runs_to_hist<64, true>(a, mine, lane, nodes, lmax);
 }
 
-// Dense tiles whose every block's nonzero values span fewer than 64 integers
-// (q50 natural or noise content): no sort.  Lane b counts its values in 64
-// 8-bit counters (value - min) in its LDS column past the histogram (16 dwords,
-// dword k*64 + lane: conflict-free, ds_add_u32), then each nonzero counter is
-// one distinct value of that frequency.  ~850 VALU per 64 blocks against ~1 470
-// for the 64-network and its run scan.
-constexpr int kHufCnt = 8192;  // byte offset of the counters in the wave's LDS (after the histogram)
-
-__device__ __forceinline__ int32_t coef_at(const uint32_t (&d)[32], int i) {
-    return (i & 1) ? (int32_t)d[i >> 1] >> 16 : (int32_t)(int16_t)(d[i >> 1] & 0xFFFFu);
-}
-
-__device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin, uint32_t &nodes, uint32_t &lmax) {
+// Tiles whose every block's values (zeros included) span fewer than 64 integers
+// (q50 noise, most natural content): no sort, and a merge in the shared byte
+// region (kHufCtrBytes), left zeroed for the next tile:
+//  1. count: one v_pk_add_u16 per coefficient pair (slot = value - vmin) and one
+//     v_perm + ds_add per coefficient;
+//  2. zeros are not symbols -- except one 0 when c[63] == 0 -- so the zero
+//     counter is replaced with last_zero;
+//  3. readout: each counter is read AND cleared by one ds_and_rtn (the wave's
+//     byte only), and adds one leaf at its frequency to the weight histogram
+//     (row 0 absorbs empty counters);
+//  4. merge as in the dense path (each lane jumps to its next occupied bucket),
+//     every bucket read AND cleared as it is processed.
+// Returns the symbol count and the WPL.
+__device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lane, int wv, int32_t vmin,
+                                            bool last_zero, uint32_t &count, uint32_t &wpl) {
     uint32_t d[32];
     tile_row(mine, lane, d);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the row is in registers before the tile is overwritten
-    __builtin_amdgcn_wave_barrier();
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t base = (uint32_t)(lane * 4);  // byte 0 of the lane's dword in every row
+    const uint32_t sh = 8u * (uint32_t)wv, inc = 1u << sh, keep = ~(0xFFu << sh);  // the wave's byte of it
+    const u16x2 off = {(unsigned short)(-vmin), (unsigned short)(-vmin)};
+    auto at = [&](uint32_t row) { return reinterpret_cast<uint32_t *>(ctr + (row << 8) + base); };
 #pragma unroll
-    for (int k = 0; k < 12; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
-    __builtin_amdgcn_wave_barrier();
-    char *cnt = mine + kHufCnt + lane * 4;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        const int32_t v = coef_at(d, i);
-        const uint32_t s = (uint32_t)(v - vmin) & 63u;
-        __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(cnt + (s >> 2) * 256), (v != 0 ? 1u : 0u) << (8 * (s & 3)),
+    for (int k = 0; k < 32; ++k) {
+        const uint32_t sl = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, d[k]) + off);  // slots, < 64 each
+        __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(ctr + __builtin_amdgcn_perm(sl, base, 0x0C0C0400u)), inc,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(ctr + __builtin_amdgcn_perm(sl, base, 0x0C0C0600u)), inc,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
-    __builtin_amdgcn_wave_barrier();
+    // zeros: their count gives the symbol count; then only c[63] == 0 leaves one
+    uint32_t zeros = 0;
+    if (vmin <= 0 && vmin > -64) {
+        const uint32_t z = (uint32_t)(-vmin);
+        zeros = (__hip_atomic_fetch_and(at(z), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+        if (last_zero) __hip_atomic_fetch_add(at(z), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    count = 64u - zeros + (last_zero ? 1u : 0u);
+    // readout (read + clear) -> weight histogram in the same rows; a row is read before any
+    // leaf can land in it only if its weight is above the rows still to read -- so the
+    // leaves go to a second set of rows: weight w at row 64 - ... no: rows are reused in
+    // order, see below
+    uint32_t lmax = 0;
+    uint32_t f[64];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint32_t w = *reinterpret_cast<const uint32_t *>(cnt + k * 256);
+    for (int s_ = 0; s_ < 64; ++s_)
+        f[s_] = (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const uint32_t f = (w >> (8 * b)) & 0xFFu;
-            hist_add(mine, f ? f : 1u, lane, f ? 1u : 0u);  // branch-free (an add of 0 for an empty counter)
-            lmax = f > lmax ? f : lmax;
-            nodes += f ? 1u : 0u;
+    for (int s_ = 0; s_ < 64; ++s_) {
+        lmax = f[s_] > lmax ? f[s_] : lmax;
+        __hip_atomic_fetch_add(at(f[s_]), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    (void)__hip_atomic_fetch_and(at(0), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);  // row 0: the empties
+    auto take = [&](uint32_t w) {  // bucket w's count, cleared
+        return (__hip_atomic_fetch_and(at(w), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+    };
+    auto peek = [&](uint32_t w) { return (*at(w) >> sh) & 0xFFu; };
+    uint64_t occ = 0;
+#pragma unroll
+    for (uint32_t w = 1; w <= 8; ++w) occ |= peek(w) ? 1ull << (w - 1) : 0ull;
+    for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w) occ |= (w <= lmax && peek(w)) ? 1ull << (w - 1) : 0ull;
+    uint32_t pending = 0;
+    wpl = 0;
+    for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ != 0); ++step) {
+        if (occ) {
+            const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
+            occ &= occ - 1ull;
+            uint32_t c = take(w);
+            if (pending && c) {
+                const uint32_t nw = pending + w;
+                wpl += nw;
+                __hip_atomic_fetch_add(at(nw), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                occ |= 1ull << (nw - 1);
+                --c;
+                pending = 0;
+            }
+            const uint32_t pairs = c >> 1;
+            if (pairs) {
+                wpl += pairs * 2 * w;
+                __hip_atomic_fetch_add(at(2 * w), pairs << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                occ |= 1ull << (2 * w - 1);
+            }
+            if (c & 1) pending = w;
         }
     }
 }
@@ -226,10 +286,15 @@ __device__ __forceinline__ void dense_counts(char *mine, int lane, int32_t vmin,
 #endif
 __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                    uint32_t *__restrict__ bits, long long ntiles) {
-    // per wave: the tile stage (9 KiB), then the histogram (8 KiB) and the dense counters (4 KiB)
+    // per wave: the tile stage (9 KiB), reused for the histogram; per workgroup: the narrow path's counters
     __shared__ uint4 lds[kHufWaves * kHufWaveLds / 16];
+    __shared__ uint4 ctr_lds[kHufCtrBytes / 16];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     char *mine = reinterpret_cast<char *>(lds) + wv * kHufWaveLds;
+    char *ctr = reinterpret_cast<char *>(ctr_lds);
+    // the narrow path leaves its rows cleared after every tile; LDS starts undefined
+    for (int i = threadIdx.x; i < kHufCtrBytes / 16; i += kHufThreads) ctr_lds[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
     const long long stride = (long long)gridDim.x * kHufWaves;
     for (long long t = (long long)blockIdx.x * kHufWaves + wv; t < ntiles; t += stride) {
         const long long left = nblk - t * 64;
@@ -252,14 +317,26 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
             *reinterpret_cast<uint4 *>(mine + (8 * k + (lane >> 3)) * kHufPitch + (lane & 7) * 16) = q[k];
         __builtin_amdgcn_wave_barrier();
         uint32_t nz = 0;
-        bool last_zero;  // c[63] == 0: value 0 is a symbol once
-        bool narrow = false;  // dense tile whose every block's values span < 64 integers
+        bool last_zero;     // c[63] == 0: value 0 is a symbol once
+        bool narrow = false;  // a dense tile whose every block has its values (zeros included) within 64 integers
         int32_t vmin = 0;
         {
             uint32_t d[32];
             tile_row(mine, lane, d);
+            {
+                // nonzeros: unsigned min(h, 1) is 1 for any nonzero half; two packed 16-bit partial sums
+                typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+                const u2 one = {1, 1};
+                u2 acc = {0, 0};
+                const uint32_t one32 = __builtin_bit_cast(uint32_t, one);
 #pragma unroll
-            for (int k = 0; k < 32; ++k) nz += ((d[k] & 0xFFFFu) != 0u) + ((d[k] >> 16) != 0u);
+                for (int k = 0; k < 32; ++k) {
+                    uint32_t m;  // inline asm: LLVM turns the packed min into compares and selects
+                    asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d[k]), "v"(one32));
+                    acc += __builtin_bit_cast(u2, m);
+                }
+                nz = (uint32_t)acc.x + (uint32_t)acc.y;
+            }
             last_zero = (d[31] >> 16) == 0u;
             if (__builtin_amdgcn_ballot_w64(nz > 32)) {
                 // dense tile: the span of its values, zeros included (packed 16-bit min/max)
@@ -280,76 +357,78 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
         // (and holding) these 32 registers across the choice
         asm volatile("" ::: "memory");
         // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
-        const uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
+        uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
         uint32_t nodes = last_zero ? 1u : 0u;
         uint32_t lmax = last_zero ? 1u : 0u;  // the largest leaf weight (dense paths)
+        const bool dense = __builtin_amdgcn_ballot_w64(nz > 32) != 0;
 #ifdef DCTQ_HUF_UNIFORM_MERGE
         const bool lane_merge = false;
 #else
-        const bool lane_merge = __builtin_amdgcn_ballot_w64(nz > 32) != 0;  // the dense paths mark occ
+        const bool lane_merge = dense;  // the dense paths merge per lane (occupancy mask)
 #endif
 #ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
         if (true) {
         } else
 #endif
-        if (!__builtin_amdgcn_ballot_w64(nz > 16))
-            sparse_runs<16>(mine, lane, nodes, lmax);
-        else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-            sparse_runs<32>(mine, lane, nodes, lmax);
-        else if (narrow)
-            dense_counts(mine, lane, vmin, nodes, lmax);
-        else
-            dense_runs(mine, lane, nodes, lmax);
-        if (last_zero) hist_add(mine, 1, lane, 1);
-        // ---- bucket merge (see the header): wpl = sum of internal node weights.
         uint32_t wpl = 0, pending = 0;
+        if (narrow) {
+            narrow_tile(mine, ctr, lane, wv, vmin, last_zero, count, wpl);  // the zero leaf included
+        } else {
+            if (!__builtin_amdgcn_ballot_w64(nz > 16))
+                sparse_runs<16>(mine, lane, nodes, lmax);
+            else if (!__builtin_amdgcn_ballot_w64(nz > 32))
+                sparse_runs<32>(mine, lane, nodes, lmax);
+            else
+                dense_runs(mine, lane, nodes, lmax);
+            if (last_zero) hist_add(mine, 1, lane, 1);
+        // ---- bucket merge (see the header): wpl = sum of internal node weights.
         if (lane >= nb) nodes = 1;  // past the tail: nothing to do
-        const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [(w-1)*64]
-        uint64_t occ = 0;
+        const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [w*64]
         if (lane_merge) {
             // occupancy of the leaf buckets, read back up to the wave's largest leaf weight
             // (cheaper than marking every leaf; this wave's LDS atomics are already ordered)
+            uint64_t occ = 0;
 #pragma unroll
             for (uint32_t w = 1; w <= 8; ++w)  // independent reads, in flight together
-                occ |= bucket[(w - 1) * 64] ? 1ull << (w - 1) : 0ull;
+                occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
             for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w)
-                occ |= bucket[(w - 1) * 64] ? 1ull << (w - 1) : 0ull;
-        // Dense tiles: each lane jumps to its own next occupied bucket (lowest bit of occ), so the
-        // loop runs as many steps as the busiest lane has occupied buckets, not up to
-        // its largest weight.  New weights (pending + w, 2w) are above w, so the
-        // scan order is the bucket order.  Every step merges at least one pair of a
-        // consistent histogram; the step cap only bounds the loop.
-        for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(nodes > 1); ++step) {
-            if (nodes > 1) {
-                const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
-                occ &= occ - 1ull;  // bucket w is emptied by this step
-                uint32_t c = w <= 64u ? bucket[(w - 1) * 64] : 0u;
-                if (pending && c) {
-                    const uint32_t nw = pending + w;
-                    wpl += nw;
-                    hist_add(mine, nw, lane, 1);
-                    mark(occ, nw, 1);
-                    --c;
-                    --nodes;
-                    pending = 0;
+                occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
+            if (lane >= nb) occ = 0;  // past the tail (the narrow path keeps them: it must clear its rows)
+            // Each lane jumps to its own next occupied bucket (lowest bit of occ), so the
+            // loop runs as many steps as the busiest lane has occupied buckets, not up to
+            // its largest weight.  New weights (pending + w, 2w) are above w, so the scan
+            // order is the bucket order; weights never exceed the symbol count (<= 64).
+            // The lane is done when no bucket is left: its last node (the root) is then
+            // `pending`.  The step cap only bounds the loop.
+            for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ != 0); ++step) {
+                if (occ) {
+                    const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
+                    occ &= occ - 1ull;  // bucket w is emptied by this step
+                    uint32_t c = bucket[w * 64];
+                    if (pending && c) {
+                        const uint32_t nw = pending + w;
+                        wpl += nw;
+                        hist_add(mine, nw, lane, 1);
+                        mark(occ, nw, 1);
+                        --c;
+                        pending = 0;
+                    }
+                    const uint32_t pairs = c >> 1;
+                    if (pairs) {
+                        wpl += pairs * 2 * w;
+                        hist_add(mine, 2 * w, lane, pairs);
+                        mark(occ, 2 * w, 1);
+                    }
+                    if (c & 1) pending = w;
                 }
-                const uint32_t pairs = c >> 1;
-                if (pairs) {
-                    wpl += pairs * 2 * w;
-                    nodes -= pairs;
-                    hist_add(mine, 2 * w, lane, pairs);
-                    mark(occ, 2 * w, 1);
-                }
-                if (c & 1) pending = w;
             }
-        }
         } else {
         // Sparse tiles (few weights): every weight in turn; bucket w+1 is read at the top of iteration w, so its
         // LDS latency hides behind the iteration; the only merges of iteration w that
         // land on w+1 (pending 1 + w, and the pairs of w = 1) are carried in a register
-        uint32_t cur = bucket[0];
+        uint32_t cur = bucket[64];
         for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
-            const uint32_t nxt = w < 64 ? bucket[w * 64] : 0u;
+            const uint32_t nxt = w < 64 ? bucket[(w + 1) * 64] : 0u;
             uint32_t c = cur, carry = 0;
             if (nodes > 1) {
                 if (pending && c) {
@@ -377,6 +456,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
             cur = nxt + carry;
         }
         }
+        }
         const __amdgpu_buffer_rsrc_t rb =
             __builtin_amdgcn_make_buffer_rsrc(bits + t * 64, (short)0, nb * 4, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b32(8u * count + wpl, rb, lane * 4, 0, 0);
@@ -386,7 +466,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
 hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bits, hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
     long long grid = (ntiles + kHufWaves - 1) / kHufWaves;
-    const long long cap = (long long)num_cus * 8;
+    const long long cap = (long long)num_cus * 8;  // 3 resident per CU (LDS-bound); the rest queue behind them
     if (grid > cap) grid = cap;
     hipLaunchKernelGGL(huffman_bits_kernel, dim3((unsigned)grid), dim3(kHufThreads), 0, stream, coef, nblk, bits,
                        ntiles);

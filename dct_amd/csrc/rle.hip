@@ -27,7 +27,6 @@ namespace dctq {
 #endif
 constexpr int kRleWaves = 4;
 constexpr int kRleThreads = 64 * kRleWaves;
-constexpr int kGroup = 8;  // decode: blocks whose symbol loads are in flight together
 
 __device__ __forceinline__ uint64_t lane_mask_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
@@ -211,7 +210,7 @@ constexpr uint8_t kZzStatic[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 2
                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 constexpr int kEmitPitch = 144;  // LDS bytes per block (128 + 16: lane-per-block row reads are conflict-free)
 constexpr int kEmitLds = 64 * kEmitPitch;
-#ifdef DCTQ_RLE_WAVE_ONLY  // A/B switch (tools/rle_ab.py): every emit/decode tile takes the wave-per-block path
+#ifdef DCTQ_RLE_WAVE_ONLY  // A/B switch (tools/rle_ab.py): emit tiles take the wave path, decode halves the quad path
 constexpr uint32_t kLaneWalkMax = 0;
 #else
 #ifndef DCTQ_EMIT_WALK_MAX
@@ -359,15 +358,14 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
 // ---- decode: one wave per 64-block tile, rebuilt 32 blocks at a time in a
 // natural-order LDS copy (8 waves/SIMD) and written as 1 KiB stores (8
 // lane-addresses per block).  Each half takes one of three paths by its symbol
-// count: lane (<= 240), walk (<= DCTQ_DEC_WALK_MAX), or scan-and-scatter, which
-// follows.  Scan path, per block: its symbols (lane s = symbol
-// s, one load; the next group's loads are issued before this group is
-// scattered), an inclusive scan of run+1 gives each symbol's zigzag position
-// (run_length_decode: pos += run; zigzag[pos++] = value, dropped past the end,
-// src/entropy.c:327-351), and the value is scattered to its natural index
-// (zigzag_to_block, :183-210, through an LDS copy of the order).  Each half
-// tile's LDS work starts after a vmcnt(0) that retires the previous half's
-// stores (store-data hazard); no store is issued inside the half.
+// count: lane (<= 240), walk (<= DCTQ_DEC_WALK_MAX) or quad (denser halves);
+// all three place each symbol at zigzag position pos (run_length_decode: pos +=
+// run; zigzag[pos++] = value, dropped past the end, src/entropy.c:327-351) of
+// its block's natural-order row (zigzag_to_block, :183-210, through an LDS copy
+// of the order).  Every symbol load goes through a buffer descriptor whose
+// num_records ends at the half's last symbol, so no path reads past the
+// stream.  Each half tile's LDS work starts after a vmcnt(0) that retires the
+// previous half's stores (store-data hazard); no store is issued inside the half.
 constexpr int kHalf = 32;
 #ifndef DCTQ_DEC_WALK_MAX
 #define DCTQ_DEC_WALK_MAX 1024
@@ -377,35 +375,6 @@ constexpr int kHalf = 32;
 // of the tile's symbols (lane 64 does not exist, and readlane(64) would wrap).
 __device__ __forceinline__ uint32_t off_at(uint32_t offv, uint32_t oend, int b) {
     return b < 64 ? __builtin_amdgcn_readlane(offv, b) : oend;
-}
-
-__device__ __forceinline__ void decode_loads(const uint32_t *symbols, uint32_t offv, uint32_t oend, int g, int nb,
-                                             int lane, uint32_t (&sy)[kGroup], uint32_t (&cnt)[kGroup]) {
-#pragma unroll
-    for (int u = 0; u < kGroup; ++u) {
-        const int jb = g + u < nb ? g + u : nb - 1;
-        const uint32_t o0 = __builtin_amdgcn_readlane(offv, jb), o1 = off_at(offv, oend, jb + 1);
-        cnt[u] = g + u < nb ? o1 - o0 : 0u;
-        sy[u] = (uint32_t)lane < cnt[u] ? symbols[o0 + lane] : 0u;
-    }
-}
-
-// Pair mode (every block of the half tile has <= 32 symbols: natural content):
-// lanes 0..31 hold block g+2u's symbols and lanes 32..63 block g+2u+1's, so
-// one load, one scan and one scatter serve two blocks.
-__device__ __forceinline__ void decode_loads_pair(const uint32_t *symbols, uint32_t offv, uint32_t oend, int g,
-                                                  int he, int lane, uint32_t (&sy)[kGroup], uint32_t (&cnt)[kGroup]) {
-    const int half = lane >> 5, s = lane & 31;
-#pragma unroll
-    for (int u = 0; u < kGroup; ++u) {
-        const int ba = g + 2 * u, bb = ba + 1;
-        const int ja = ba < he ? ba : he - 1, jb = bb < he ? bb : he - 1;
-        const uint32_t a0 = __builtin_amdgcn_readlane(offv, ja), a1 = off_at(offv, oend, ja + 1);
-        const uint32_t b0 = __builtin_amdgcn_readlane(offv, jb), b1 = off_at(offv, oend, jb + 1);
-        const uint32_t ca = ba < he ? a1 - a0 : 0u, cb = bb < he ? b1 - b0 : 0u;
-        cnt[u] = half ? cb : ca;
-        sy[u] = (uint32_t)s < cnt[u] ? symbols[(half ? b0 : a0) + s] : 0u;
-    }
 }
 
 // Walk path (a half tile of at most kDecWalkMax symbols): lane i < 32 rebuilds
@@ -432,10 +401,6 @@ constexpr uint32_t kDecLaneMax = 240, kDecWalkMax = DCTQ_DEC_WALK_MAX;
 #endif
 constexpr int kDecPitch = 144;
 constexpr int kDecBatch = 16;  // symbols per lane per step
-#ifndef DCTQ_DEC_QUAD
-#define DCTQ_DEC_QUAD 1
-#endif
-constexpr bool kDecQuad = DCTQ_DEC_QUAD;  // halves above the walk path: the quad path instead of the scan path
 constexpr int kDecLds = kHalf * 128 + 240 * 4;  // >= kHalf * kDecPitch
 static_assert(kDecLds >= kHalf * kDecPitch, "walk path tile");
 
@@ -463,7 +428,6 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
             const uint32_t s0 = __builtin_amdgcn_readlane(offv, h), nh = off_at(offv, oend, he) - s0;
             const bool lane_path = kDecLaneMax && nh <= kDecLaneMax;
             const bool walk = !lane_path && kDecWalkMax && nh <= kDecWalkMax;
-            const bool quad = kDecQuad && !lane_path && !walk;
             if (lane_path) {
                 const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
@@ -535,7 +499,7 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
 #pragma unroll
                     for (int k = 0; k < kDecBatch / 4; ++k) cur[k] = nxt[k];
                 }
-            } else if (quad) {
+            } else {
                 // Quad path: 4 blocks per step, one per 16-lane row; lane s of a row holds its
                 // block's symbols 4s..4s+3 (one 16-B load: 4 symbols per lane-address). Positions:
                 // a 4-element prefix in the lane, then a row-segmented DPP scan of the lane totals.
@@ -587,64 +551,11 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
                     q = nq;
                     cnt = ncnt;
                 }
-            } else {
-                const bool pair = !__builtin_amdgcn_ballot_w64(lane >= h && lane < he && cnt_lane > 32u);
-                uint32_t sy[kGroup], cnt[kGroup];
-                if (pair)
-                    decode_loads_pair(symbols, offv, oend, h, he, lane, sy, cnt);
-                else
-                    decode_loads(symbols, offv, oend, h, nb, lane, sy, cnt);
-                __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the previous half's stores, before any LDS read
-#pragma unroll
-                for (int k = 0; k < 4; ++k) reinterpret_cast<u4r *>(lt)[k * 64 + lane] = u4r{0u, 0u, 0u, 0u};
-                if (pair) {
-                    const int half = lane >> 5, s = lane & 31;
-                    for (int g = h; g < he; g += 2 * kGroup) {
-                        uint32_t nsy[kGroup], ncnt[kGroup];
-                        decode_loads_pair(symbols, offv, oend, g + 2 * kGroup < he ? g + 2 * kGroup : g, he, lane,
-                                          nsy, ncnt);
-#pragma unroll
-                        for (int u = 0; u < kGroup; ++u) {
-                            const bool live = (uint32_t)s < cnt[u];
-                            uint32_t e = wave_inclusive_scan(live ? (sy[u] >> 16) + 1u : 0u);
-                            const uint32_t lo = __builtin_amdgcn_readlane(e, 31);  // block A's total
-                            if (half) e -= lo;
-                            const uint32_t pos = e - 1u;
-                            const int b = g + 2 * u + half;
-                            if (live && pos < 64u && b < he)
-                                *reinterpret_cast<int16_t *>(lt + (b - h) * 128 + 2 * zz[pos]) =
-                                    (int16_t)(sy[u] & 0xFFFFu);
-                        }
-#pragma unroll
-                        for (int u = 0; u < kGroup; ++u) {
-                            sy[u] = nsy[u];
-                            cnt[u] = ncnt[u];
-                        }
-                    }
-                } else
-                    for (int g = h; g < he; g += kGroup) {
-                        uint32_t nsy[kGroup], ncnt[kGroup];
-                        decode_loads(symbols, offv, oend, g + kGroup < he ? g + kGroup : g, nb, lane, nsy, ncnt);
-#pragma unroll
-                        for (int u = 0; u < kGroup; ++u) {
-                            const uint32_t e =
-                                wave_inclusive_scan((uint32_t)lane < cnt[u] ? (sy[u] >> 16) + 1u : 0u);
-                            const uint32_t pos = e - 1u;
-                            if ((uint32_t)lane < cnt[u] && pos < 64u && g + u < he)
-                                *reinterpret_cast<int16_t *>(lt + (g - h + u) * 128 + 2 * zz[pos]) =
-                                    (int16_t)(sy[u] & 0xFFFFu);
-                        }
-#pragma unroll
-                        for (int u = 0; u < kGroup; ++u) {
-                            sy[u] = nsy[u];
-                            cnt[u] = ncnt[u];
-                        }
-                    }
             }
             wave_sync_lds();
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the walk's last (clipped) loads before the read-out
             u4r val[4];
-            const int pitch = walk || quad ? kDecPitch : 128;
+            const int pitch = lane_path ? 128 : kDecPitch;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 val[k] = *reinterpret_cast<const u4r *>(lt + (8 * k + (lane >> 3)) * pitch + 16 * (lane & 7));
