@@ -234,7 +234,8 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
         const uint32_t n = qb[slot], e = qc[slot];
         const int c = (int)(e & 63u);
         const int val = exact_entry<ADAPTIVE>(ring + slot * 4, c, dev);
-        coef_of(ps, e >> 6)[(size_t)n * 64 + c] = (int16_t)val;
+        if (DCTQ_ABLATE & 4096) asm volatile("" ::"v"(val));  // diagnostic: computed, not patched
+        else coef_of(ps, e >> 6)[(size_t)n * 64 + c] = (int16_t)val;
     }
     qn -= take;
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);

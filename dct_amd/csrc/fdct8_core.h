@@ -93,7 +93,7 @@ constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) con
 #define DCTQ_LOAD_NT 1  // pixel rows are read exactly once
 #endif
 #ifndef DCTQ_ABLATE
-#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores, 2048 no final drain
+#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores, 2048 no final drain, 4096 drains compute but do not patch
 #endif
 
 template <int K>
