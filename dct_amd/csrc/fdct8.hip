@@ -233,9 +233,10 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
         const int slot = qn - take + lane;
         const uint32_t n = qb[slot], e = qc[slot];
         const int c = (int)(e & 63u);
-        const int val = exact_entry<ADAPTIVE>(ring + slot * 4, c, dev);
+        const int val = exact_entry<ADAPTIVE>(ring + (e >> 9) * 4, c, dev);
         if (DCTQ_ABLATE & 4096) asm volatile("" ::"v"(val));  // diagnostic: computed, not patched
-        else coef_of(ps, e >> 6)[(size_t)n * 64 + c] = (int16_t)val;
+        else if (!DCTQ_PATCH_COND || (((uint32_t)val ^ (e >> 8)) & 1u))
+            coef_of(ps, (e >> 6) & 3u)[(size_t)n * 64 + c] = (int16_t)val;
     }
     qn -= take;
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
@@ -323,24 +324,33 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     if (!valid || (DCTQ_ABLATE & 8)) mlo = mhi = 0;
     if (DCTQ_ABLATE & 32) asm volatile("" : "+v"(mlo), "+v"(mhi), "+s"(qn));  // keep code, never run (diagnostic)
     uint64_t has = __builtin_amdgcn_ballot_w64((DCTQ_ABLATE & 32) ? (mlo == 0x12345u && mhi == 0x6789u) : (mlo | mhi) != 0);
+    const int16_t *mine16 = reinterpret_cast<const int16_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 2);
+    int sfirst = -1;  // ring slot holding this lane's pixels for this batch's entries
     while (has) {
         if (qn > kQCap - 64) {
             if (DCTQ_ABLATE & 16) qn = 0;
             else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
+            sfirst = -1;  // the drained slots are reused from here on
         }
         if (mlo | mhi) {
             const int c = pop_flag(mlo, mhi);
             const uint32_t pos =
                 qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
+            const bool fresh = !DCTQ_STASH_DEDUP || sfirst < 0;
+            const uint32_t s = fresh ? pos : (uint32_t)sfirst;
             qb[pos] = n;
-            qc[pos] = (uint16_t)((uint32_t)c | ((uint32_t)k << 6));
+            // entry: coefficient | plane << 6 | parity of the stored fast value << 8 | stash slot << 9
+            qc[pos] = (uint16_t)((uint32_t)c | ((uint32_t)k << 6) | (((uint32_t)mine16[c] & 1u) << 8) | (s << 9));
             // stash the block's pixels while they are still in registers: the
             // drain must not go back to HBM for them (8 random 64-B bursts per entry)
-            uint4 *st = ring + pos * 4;
-            if (!(DCTQ_ABLATE & 1024))
+            if (fresh) {
+                uint4 *st = ring + pos * 4;
+                sfirst = (int)pos;
+                if (!(DCTQ_ABLATE & 1024))
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    st[k] = make_uint4(cur[2 * k].x, cur[2 * k].y, cur[2 * k + 1].x, cur[2 * k + 1].y);
+                    for (int k = 0; k < 4; ++k)
+                        st[k] = make_uint4(cur[2 * k].x, cur[2 * k].y, cur[2 * k + 1].x, cur[2 * k + 1].y);
+            }
         }
         qn += __builtin_popcountll(has);
         has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
