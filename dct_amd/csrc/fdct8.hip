@@ -197,7 +197,10 @@ __global__ __launch_bounds__(kThreads) void fdct8_quant_v1(PlaneArgs p, FastTabl
 //  * the LDS stage is written out as 1 KiB-contiguous buffer stores (num_records
 //    clips the tail, so the stores are unconditional);
 //  * flagged (block, coefficient) pairs go to a wave-local LDS queue and are
-//    recomputed exactly 64 at a time (every lane busy), then patched in HBM;
+//    recomputed exactly 64 at a time (every lane busy), then patched in HBM
+//    where the result changes; a full queue drains at the next batch, before
+//    that batch's stores are issued (vmcnt is one in-order counter: behind
+//    8 KiB of fresh stores, the drain's stash loads would wait for all of them);
 //  * one launch covers up to 4 planes (PlaneSet): the grid-stride index runs
 //    over the concatenated 64-block batches, each batch finding its plane by
 //    wave-uniform compares against the planes' batch prefixes.
@@ -221,7 +224,12 @@ __device__ int exact_entry(const uint4 *__restrict__ stash, int c, const DevTabl
 }
 
 // Exact recomputation of up to 64 queued (block, coefficient) entries, one per
-// lane, patched into their planes' coefficient arrays.
+// lane, patched into their planes' coefficient arrays where the exact value
+// differs from the fast one already stored (the two differ by at most 1 inside
+// the guard band, so the parity bit kept in the entry decides).  A 2-B patch
+// into a line already written back costs a read-modify-write at the memory
+// (~155 B of stream time, profiles/r02/forward_overheads.md), so skipping the
+// ~half of them that would rewrite the same value is the cheapest patch.
 template <bool ADAPTIVE, bool STATS>
 __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables *__restrict__ dev, const uint32_t *qb,
                                             const uint16_t *qc, const uint4 *ring, int &qn, int lane,
@@ -229,18 +237,32 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
     // the wave's own coefficient stores (and its stash stores) must land first
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     const int take = qn < 64 ? qn : 64;
+    // the planes' output pointers in SGPRs: selected per lane with v_cndmask (left
+    // to itself the compiler indexes the kernel-argument array with a per-lane
+    // global load, one more memory latency in front of every patch)
+    int16_t *cp[kMaxPlanes];
+#pragma unroll
+    for (int i = 0; i < kMaxPlanes; ++i) {
+        cp[i] = ps.coef[i];
+        asm volatile("" : "+s"(cp[i]));
+    }
     if (lane < take) {
         const int slot = qn - take + lane;
         const uint32_t n = qb[slot], e = qc[slot];
         const int c = (int)(e & 63u);
         const int val = exact_entry<ADAPTIVE>(ring + (e >> 9) * 4, c, dev);
-        if (DCTQ_ABLATE & 4096) asm volatile("" ::"v"(val));  // diagnostic: computed, not patched
-        else if (!DCTQ_PATCH_COND || (((uint32_t)val ^ (e >> 8)) & 1u))
-            coef_of(ps, (e >> 6) & 3u)[(size_t)n * 64 + c] = (int16_t)val;
+        if (DCTQ_ABLATE & 4096) {
+            asm volatile("" ::"v"(val));  // diagnostic: computed, not patched
+        } else if (!DCTQ_PATCH_COND || (((uint32_t)val ^ (e >> 8)) & 1u)) {
+            const uint32_t k = (e >> 6) & 3u;
+            int16_t *dst = cp[0];
+#pragma unroll
+            for (int i = 1; i < kMaxPlanes; ++i) dst = k == (uint32_t)i ? cp[i] : dst;
+            ((__attribute__((address_space(1))) int16_t *)dst)[(size_t)n * 64 + c] = (int16_t)val;
+        }
     }
     qn -= take;
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // nothing of this rare path stays in flight
 }
 
 // One 64-block batch of the v2 loop.  `nxt` holds this batch's rows on entry and
@@ -281,6 +303,14 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     // counter for loads and stores) also drains this batch's stores.
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+
+    // A full round of entries from earlier batches drains HERE, before this
+    // batch's stores are issued: vmcnt counts in issue order, so a drain after
+    // them would wait for all 8 KiB of them before its first stash load returns.
+    if (qn >= 64) {
+        if (DCTQ_ABLATE & 16) qn = 0;
+        else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
+    }
 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -354,10 +384,6 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
         }
         qn += __builtin_popcountll(has);
         has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
-    }
-    if (qn >= 64) {
-        if (DCTQ_ABLATE & 16) qn = 0;
-        else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
     }
 }
 
