@@ -40,6 +40,10 @@
 // DCTQ_HUF_MIN_WAVES (launch bound, default 3 waves/SIMD: 168 VGPRs) is an A/B knob.
 #include "dctq_internal.h"
 
+#ifndef DCTQ_HUF_ABLATE
+#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge
+#endif
+
 namespace dctq {
 
 constexpr int kHufWaves = 4;
@@ -207,7 +211,7 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
 //  4. merge as in the dense path (each lane jumps to its next occupied bucket),
 //     every bucket read AND cleared as it is processed.
 // Returns the symbol count and the WPL.
-__device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lane, int wv, int32_t vmin,
+__device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lane, int wv, int32_t vmin, uint32_t span,
                                             bool last_zero, uint32_t &count, uint32_t &wpl) {
     uint32_t d[32];
     tile_row(mine, lane, d);
@@ -232,20 +236,41 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
         if (last_zero) __hip_atomic_fetch_add(at(z), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
     count = 64u - zeros + (last_zero ? 1u : 0u);
-    // readout (read + clear) -> weight histogram in the same rows; a row is read before any
-    // leaf can land in it only if its weight is above the rows still to read -- so the
-    // leaves go to a second set of rows: weight w at row 64 - ... no: rows are reused in
-    // order, see below
+    // readout: every counter read and cleared, THEN the leaves added (the weight
+    // histogram reuses the rows).  Only rows below the wave's largest span hold
+    // counts (q50 noise: 32 of 64), in wave-uniform chunks of 8 rows.
     uint32_t lmax = 0;
     uint32_t f[64];
 #pragma unroll
-    for (int s_ = 0; s_ < 64; ++s_)
-        f[s_] = (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+    for (int c8 = 0; c8 < 8; ++c8) {
+        if (c8 == 0 || __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8))) {
 #pragma unroll
-    for (int s_ = 0; s_ < 64; ++s_) {
-        lmax = f[s_] > lmax ? f[s_] : lmax;
-        __hip_atomic_fetch_add(at(f[s_]), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_)
+                f[s_] = (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+        } else {
+#pragma unroll
+            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) f[s_] = 0;
+        }
     }
+#if DCTQ_HUF_ABLATE == 1  // timing: count + readout only
+    wpl = f[0] + f[63];
+    return;
+#endif
+#pragma unroll
+    for (int c8 = 0; c8 < 8; ++c8) {
+        if (c8 == 0 || __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8))) {
+#pragma unroll
+            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) {
+                lmax = f[s_] > lmax ? f[s_] : lmax;
+                __hip_atomic_fetch_add(at(f[s_]), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+        }
+    }
+#if DCTQ_HUF_ABLATE == 2  // timing: leaf adds, then a plain clear instead of the merge
+#pragma unroll
+    for (int s_ = 0; s_ < 65; ++s_) wpl += (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+    return;
+#endif
     (void)__hip_atomic_fetch_and(at(0), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);  // row 0: the empties
     auto take = [&](uint32_t w) {  // bucket w's count, cleared
         return (__hip_atomic_fetch_and(at(w), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
@@ -320,6 +345,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
         bool last_zero;     // c[63] == 0: value 0 is a symbol once
         bool narrow = false;  // a dense tile whose every block has its values (zeros included) within 64 integers
         int32_t vmin = 0;
+        uint32_t span = 64;  // the lane's values (zeros included) lie in [vmin, vmin + span)
         {
             uint32_t d[32];
             tile_row(mine, lane, d);
@@ -350,6 +376,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
                 }
                 vmin = mn.x < mn.y ? mn.x : mn.y;
                 const int32_t vmax = mx.x > mx.y ? mx.x : mx.y;
+                span = (uint32_t)(vmax - vmin + 1);
                 narrow = !__builtin_amdgcn_ballot_w64(lane < nb && vmax - vmin >= 64);
             }
         }
@@ -372,7 +399,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
 #endif
         uint32_t wpl = 0, pending = 0;
         if (narrow) {
-            narrow_tile(mine, ctr, lane, wv, vmin, last_zero, count, wpl);  // the zero leaf included
+            narrow_tile(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl);  // the zero leaf included
         } else {
             if (!__builtin_amdgcn_ballot_w64(nz > 16))
                 sparse_runs<16>(mine, lane, nodes, lmax);
