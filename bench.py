@@ -80,6 +80,10 @@ def parse():
                     help="timed steps of the config-5 round trip leg (forward+inverse, PSNR); 0 = skip")
     ap.add_argument("--ceiling-rounds", type=int, default=10,
                     help="interleaved forward / no-arithmetic movement launches for roofline.movement_ceiling (0 = skip)")
+    ap.add_argument("--prewarm-ms", type=float, default=250.0,
+                    help="untimed GPU pre-warm before the warmup steps: the step runs back to back for this long so "
+                         "the timed steps see steady-state clocks (an idle MI355X sits at ~100 MHz sclk and needs "
+                         "~25 ms of load to ramp: profiles/r02/clock_ramp.md)")
     ap.add_argument("--per-plane", action="store_true",
                     help="two launches per step (luma, then chroma) instead of one multi-plane launch")
     ap.add_argument("--backend", default="nccl", help="N>1 process group (nccl = RCCL; gloo only to rehearse "
@@ -481,21 +485,27 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
                          "adaptive=1 with Q*(2-nv)"}
 
 
-def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10):
-    """Memory ceilings of the forward kernel's traffic on THIS box, interleaved
-    with the forward launch itself (HIP events, medians), through the diagnostic
-    library (libdct_amd_diag.so, csrc/dctq_diag.h):
+def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3):
+    """Memory ceilings of the forward kernel's traffic on THIS box, measured in
+    rounds beside the forward launch itself, through the diagnostic library
+    (libdct_amd_diag.so, csrc/dctq_diag.h):
       movement_v2 : dctq_diag_movement_planes -- the forward launch's exact data
                     movement (same grid, prefetch, LDS stage, 1 KiB stores), no math;
       flat_1to2_* : dctq_diag_stream 0/1 -- the same byte counts as a flat stream
                     (16 B per lane, 1 KiB per instruction), nt / default stores;
-      read_only / write_only : dctq_diag_stream 2/3 over the same byte counts;
-      phased      : read-only then write-only, i.e. the 1:2 traffic with no mix
-                    (not reachable by one launch that transforms the data:
-                    profiles/r02/hbm_ceilings.md).
-    movement_ceiling = the best of movement_v2 and the flat streams; the forward
-    kernel's time against it is forward_over_ceiling.  Overwrites coef_y/coef_c
-    (run after the parity check)."""
+      read_only, write_only(_nt) : dctq_diag_stream 2/3/4 over the same byte counts;
+      phased_*    : a read-only launch then a write-only launch, timed as a pair,
+                    i.e. the 1:2 traffic with no mix (not reachable by one launch
+                    that transforms the data: profiles/r02/hbm_ceilings.md).
+    Steady state: every sample is `b2b` launches of one case back to back after
+    one untimed launch of the same case.  Default-policy stores leave dirty lines
+    in the caches that are written back during the NEXT launch, so timing single
+    launches in rotation charges one case's write-back to another (round 2:
+    plain stores looked 2-25 % faster than nt that way and were 4-15 % slower
+    in steady state, profiles/r02/policy_b2b.md).
+    movement_ceiling = the best 1:2 pattern; the forward kernel's time against
+    it is forward_over_ceiling.  Overwrites coef_y/coef_c (run after the parity
+    check)."""
     import statistics
     D = dct_amd.diag()
     dplan = dct_amd.Plan(args.quality, args.adaptive, diagnostic=True)
@@ -507,10 +517,11 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10):
     src.fill_(7)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def diag_stream(kind):
-        rc = D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), nflat, stream)
-        if rc:
-            raise RuntimeError(f"dctq_diag_stream({kind}) rc={rc}")
+    def diag_stream(*kinds):
+        for kind in kinds:
+            rc = D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), nflat, stream)
+            if rc:
+                raise RuntimeError(f"dctq_diag_stream({kind}) rc={rc}")
 
     cases = {
         "forward": (lambda: plan.forward_quant_planes(pls, outs=outs), nblk * BYTES_PER_BLOCK),
@@ -519,29 +530,34 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10):
         "flat_1to2_nt_plain": (lambda: diag_stream(1), nflat * BYTES_PER_BLOCK),
         "read_only": (lambda: diag_stream(2), nflat * 64),
         "write_only": (lambda: diag_stream(3), nflat * 128),
+        "write_only_nt": (lambda: diag_stream(4), nflat * 128),
+        "phased_read_then_write": (lambda: diag_stream(2, 3), nflat * BYTES_PER_BLOCK),
+        "phased_read_then_write_nt": (lambda: diag_stream(2, 4), nflat * BYTES_PER_BLOCK),
     }
     times = {k: [] for k in cases}
     for r in range(rounds + 1):
         for k, (fn, _) in cases.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            fn()  # the sample's predecessor is the same case
             e0.record()
-            fn()
+            for _ in range(b2b):
+                fn()
             e1.record()
             torch.cuda.synchronize()
             if r:
-                times[k].append(e0.elapsed_time(e1) * 1e-3)
+                times[k].append(e0.elapsed_time(e1) * 1e-3 / b2b)
     med = {k: statistics.median(v) for k, v in times.items()}
     frac = {k: cases[k][1] / med[k] / 1e9 / HBM_PEAK_GBS for k in cases}
-    phased = nflat * BYTES_PER_BLOCK / (med["read_only"] + med["write_only"]) / 1e9 / HBM_PEAK_GBS
     best = max(("movement_v2", "flat_1to2_nt_nt", "flat_1to2_nt_plain"), key=lambda k: frac[k])
     del src, dst
     return {"pattern": best, "achieved": frac[best] * HBM_PEAK_GBS, "frac": frac[best],
             "forward_frac": frac["forward"], "forward_over_ceiling": frac["forward"] / frac[best],
             "forward_over_own_movement": frac["forward"] / frac["movement_v2"], "rounds": rounds,
-            "hw_ceilings": {**{k: {"median_us": med[k] * 1e6, "frac": frac[k]} for k in cases},
-                            "phased_read_then_write": {"frac": phased,
-                                                       "note": "two kernels: an upper bound no single launch "
-                                                               "that transforms the data reaches"}}}
+            "launches_per_sample": b2b,
+            "hw_ceilings": {k: {"median_us": med[k] * 1e6, "frac": frac[k],
+                                **({"note": "two kernels: an upper bound no single launch that transforms the "
+                                            "data reaches"} if k.startswith("phased") else {})}
+                            for k in cases}}
 
 
 def traffic_for(args, launches):
@@ -609,6 +625,17 @@ def main():
         if ev is not None:
             ev[2].record()
 
+    # Clock ramp: from idle, the first ~50 launches (~25 ms) run up to 20 % slower
+    # than the steady state (tools/ramp.py).  A serving GPU is not idle, so the
+    # step runs back to back untimed until `prewarm_ms` of it has executed, then
+    # the W warmup steps, then the K timed steps.
+    prewarm_steps, t_pre = 0, time.perf_counter()
+    while args.prewarm_ms > 0 and (time.perf_counter() - t_pre) * 1e3 < args.prewarm_ms:
+        for _ in range(8):
+            step()
+        prewarm_steps += 8
+        torch.cuda.synchronize()  # the time bound counts executed work, not queued launches
+    prewarm = {"steps": prewarm_steps, "ms": (time.perf_counter() - t_pre) * 1e3}
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -675,6 +702,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm": prewarm,
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",

@@ -32,7 +32,8 @@ int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, i
  *           64-block batch, persistent grid, nt loads, nt stores;
  *   kind 1: the same with default-policy stores;
  *   kind 2: read-only stream of blocks * 64 bytes of src (nt);
- *   kind 3: write-only stream of blocks * 128 bytes of dst (default policy).
+ *   kind 3: write-only stream of blocks * 128 bytes of dst (default policy);
+ *   kind 4: the same with non-temporal stores.
  * src >= blocks * 64 bytes, dst >= blocks * 128 bytes, both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
 

@@ -43,11 +43,16 @@ __global__ __launch_bounds__(256) void stream_read(const u4v *__restrict__ src, 
     if (acc.x == 0x12345678u && acc.y == 0x9abcdef0u && acc.z == 0x0fedcba9u) sink[0] = acc;
 }
 
+template <bool NT>
 __global__ __launch_bounds__(256) void stream_write(u4v *__restrict__ dst, size_t n16) {
     const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-        if (base + u * 256 < n16) dst[base + u * 256] = u4v{(unsigned)base, (unsigned)u, 7u, 9u};
+        if (base + u * 256 < n16) {
+            const u4v v = u4v{(unsigned)base, (unsigned)u, 7u, 9u};
+            if (NT) __builtin_nontemporal_store(v, dst + base + u * 256);
+            else dst[base + u * 256] = v;
+        }
 }
 
 int device_cus() {
@@ -97,12 +102,16 @@ int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, voi
                            (u4v *)dst, n16);
         break;
     }
-    case 3: {
+    case 3:
+    case 4: {
         const size_t n16 = (size_t)blocks * 8;
-        hipLaunchKernelGGL(stream_write, dim3((unsigned)((n16 + 1023) / 1024)), dim3(256), 0, s, (u4v *)dst, n16);
+        if (kind == 3)
+            hipLaunchKernelGGL(stream_write<false>, dim3((unsigned)((n16 + 1023) / 1024)), dim3(256), 0, s, (u4v *)dst, n16);
+        else
+            hipLaunchKernelGGL(stream_write<true>, dim3((unsigned)((n16 + 1023) / 1024)), dim3(256), 0, s, (u4v *)dst, n16);
         break;
     }
-    default: return fail(DCTQ_EINVAL, "kind must be 0..3");
+    default: return fail(DCTQ_EINVAL, "kind must be 0..4");
     }
     HIPCHK(hipGetLastError(), "diag stream launch");
     return DCTQ_OK;

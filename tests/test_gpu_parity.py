@@ -291,12 +291,13 @@ def test_diag_stream_moves_bytes(T, dm):
         flip = b[:, 4:].copy().view(np.uint32)
         flip.reshape(-1, 4)[:, 0] ^= 1
         assert np.array_equal(flip.view(np.uint8).reshape(a.shape), a)
-    dst = T.zeros(n * 128, dtype=T.uint8, device="cuda")
-    assert D.dctq_diag_stream(3, src.data_ptr(), dst.data_ptr(), n, s) == 0
-    assert D.dctq_diag_stream(2, src.data_ptr(), dst.data_ptr(), n, s) == 0
-    T.cuda.synchronize()
-    w = dst.view(-1, 16).cpu().numpy().view(np.uint32)
-    assert (w[:, 2] == 7).all() and (w[:, 3] == 9).all()
+    for kind in (3, 4):
+        dst = T.zeros(n * 128, dtype=T.uint8, device="cuda")
+        assert D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), n, s) == 0
+        assert D.dctq_diag_stream(2, src.data_ptr(), dst.data_ptr(), n, s) == 0
+        T.cuda.synchronize()
+        w = dst.view(-1, 16).cpu().numpy().view(np.uint32)
+        assert (w[:, 2] == 7).all() and (w[:, 3] == 9).all()
     assert D.dctq_diag_stream(9, src.data_ptr(), dst.data_ptr(), n, s) != 0
 
 
