@@ -41,7 +41,7 @@
 #include "dctq_internal.h"
 
 #ifndef DCTQ_HUF_ABLATE
-#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge
+#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge
 #endif
 
 namespace dctq {
@@ -271,39 +271,83 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
     for (int s_ = 0; s_ < 65; ++s_) wpl += (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
     return;
 #endif
+    // ---- merge in registers (no LDS round trip inside the merge; Python model:
+    // tests/test_oracle.py::register_merge_wpl).  Leaf weights <= 16 are read back
+    // from their rows (each row read AND cleared) and scanned w = 1..16 as the
+    // bucket merge.  A pending merge makes ONE node of weight p + w in (w, 2w), and
+    // successive ones are strictly heavier, so they are bits of a mask.  Nodes
+    // heavier than 16 (leaves, pairs of w >= 9, pending merges) are at most 3,
+    // because all node weights add up to the symbol count (<= 65): their count,
+    // sum, min and max give them sorted, and with the pending node (the lightest)
+    // they finish in closed form.
     (void)__hip_atomic_fetch_and(at(0), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);  // row 0: the empties
-    auto take = [&](uint32_t w) {  // bucket w's count, cleared
+    auto take = [&](uint32_t w) {  // row w's count, cleared
         return (__hip_atomic_fetch_and(at(w), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
     };
-    auto peek = [&](uint32_t w) { return (*at(w) >> sh) & 0xFFu; };
-    uint64_t occ = 0;
+    uint32_t cnt[17];
 #pragma unroll
-    for (uint32_t w = 1; w <= 8; ++w) occ |= peek(w) ? 1ull << (w - 1) : 0ull;
-    for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w) occ |= (w <= lmax && peek(w)) ? 1ull << (w - 1) : 0ull;
-    uint32_t pending = 0;
-    wpl = 0;
-    for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ != 0); ++step) {
-        if (occ) {
-            const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
-            occ &= occ - 1ull;
-            uint32_t c = take(w);
-            if (pending && c) {
-                const uint32_t nw = pending + w;
-                wpl += nw;
-                __hip_atomic_fetch_add(at(nw), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                occ |= 1ull << (nw - 1);
-                --c;
-                pending = 0;
-            }
-            const uint32_t pairs = c >> 1;
-            if (pairs) {
-                wpl += pairs * 2 * w;
-                __hip_atomic_fetch_add(at(2 * w), pairs << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                occ |= 1ull << (2 * w - 1);
-            }
-            if (c & 1) pending = w;
-        }
+    for (int w = 1; w <= 16; ++w) cnt[w] = take((uint32_t)w);  // independent reads, all in flight
+    // heavy nodes: count, sum, min, max
+    uint32_t hn = 0, hs = 0, hmn = 0xFFu, hmx = 0;
+    for (uint32_t r = 17; __builtin_amdgcn_ballot_w64(r <= lmax); ++r) {  // heavy leaves, rows ascending
+        const uint32_t k = take(r);
+        hn += k;
+        hs += k * r;
+        hmn = (k && hmn == 0xFFu) ? r : hmn;
+        hmx = k ? r : hmx;
     }
+#if DCTQ_HUF_ABLATE == 3  // timing: leaf adds and read-back, no merge
+    wpl = hn + hs;
+#pragma unroll
+    for (int w = 1; w <= 16; ++w) wpl += cnt[w];
+    return;
+#endif
+    uint32_t p = 0, pm = 0;  // the pending node's weight (0: none); pending-merge nodes (bit = weight)
+    uint32_t qn = 0, qs = 0, qmn = 0xFFu, qmx = 0;  // heavy pairs (weights 2w, w = 9..16, ascending)
+    wpl = 0;
+#pragma unroll
+    for (uint32_t w = 1; w <= 16; ++w) {
+        uint32_t c = cnt[w];
+        if (w >= 3) c += (pm >> w) & 1u;  // p + w' >= 3
+        const bool mp = p != 0 && c != 0;  // the pending node merges with one node of bucket w
+        const uint32_t nw = p + w;         // in (w, 2w): at most 31
+        wpl += mp ? nw : 0u;
+        c -= mp ? 1u : 0u;
+        pm |= mp ? 1u << nw : 0u;
+        p = mp ? 0u : p;
+        const uint32_t pairs = c >> 1;
+        wpl += pairs * 2 * w;
+        if (2 * w <= 16) {
+            cnt[2 * w] += pairs;
+        } else {
+            qn += pairs;
+            qs += pairs * 2 * w;
+            qmn = (pairs && qmn == 0xFFu) ? 2 * w : qmn;
+            qmx = pairs ? 2 * w : qmx;
+        }
+        p = (c & 1u) ? w : p;
+    }
+    // the pending-merge nodes above 16 (<= 3 bits of pm, bits 17..31)
+    {
+        uint32_t b = pm & ~0x1FFFFu;
+        const uint32_t n = (uint32_t)__builtin_popcount(b);
+        const uint32_t lo = b ? (uint32_t)__builtin_ctz(b) : 0xFFu, hi = b ? 31u - (uint32_t)__builtin_clz(b) : 0u;
+        const uint32_t mid = n == 3 ? (uint32_t)__builtin_ctz(b & (b - 1)) : 0u;
+        hn += n + qn;
+        hs += (n ? lo : 0u) + (n == 3 ? mid : 0u) + (n >= 2 ? hi : 0u) + qs;
+        hmn = min(min(hmn, qmn), lo);
+        hmx = max(max(hmx, qmx), hi);
+    }
+    // the heavy nodes sorted: h1 <= h2 <= h3 (h2 = h3 when there are two)
+    const uint32_t h1 = hmn, h3 = hmx, h2 = hn == 3 ? hs - h1 - h3 : h3;
+    uint32_t fin;
+    if (p) {  // p < 17 <= h1: nodes p, h1, h2, h3
+        const uint32_t s2 = p + h1;
+        fin = hn == 3 ? 2 * s2 + 2 * h2 + h3 + min(s2, h3) : hn == 2 ? 2 * s2 + h2 : hn == 1 ? s2 : 0u;
+    } else {
+        fin = hn == 3 ? 2 * (h1 + h2) + h3 : hn == 2 ? h1 + h3 : 0u;
+    }
+    wpl += fin;
 }
 
 #ifndef DCTQ_HUF_MIN_WAVES
@@ -393,11 +437,11 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
 #else
         const bool lane_merge = dense;  // the dense paths merge per lane (occupancy mask)
 #endif
+        uint32_t wpl = 0, pending = 0;
 #ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
         if (true) {
         } else
 #endif
-        uint32_t wpl = 0, pending = 0;
         if (narrow) {
             narrow_tile(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl);  // the zero leaf included
         } else {

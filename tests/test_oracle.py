@@ -237,6 +237,104 @@ def test_huffman_bucket_model_is_exact():
         assert bucket_merge_bits(blk) == O.huffman_bits(blk), blk.tolist()
 
 
+def register_merge_wpl(freqs):
+    """Python model of the narrow path's register merge (dct_amd/csrc/huffman.hip,
+    narrow_tile), operation for operation:
+      * leaf weights <= 16 counted in 16 buckets; the bucket merge scans w = 1..16
+        (a pending node merges with one node of the next non-empty bucket, the rest
+        pair up);
+      * a pending merge makes ONE node of weight p + w in (w, 2w), and successive
+        ones are strictly heavier, so they are bits of a mask (bit p + w), never
+        two in one bucket;
+      * every node heavier than 16 -- leaves, pairs of w >= 9, pending merges --
+        waits aside.  All node weights add up to the symbol count (<= 65), so there
+        are at most 3 of them, and their count, sum, min and max give them sorted;
+      * the pending node (<= 16, the lightest) and those finish in closed form.
+    Returns the weighted path length (sum of internal node weights)."""
+    cnt = [0] * 17
+    hn, hs, hmn, hmx = 0, 0, 99, 0  # heavy nodes: count, sum, min, max
+
+    def heavy(k, x):
+        nonlocal hn, hs, hmn, hmx
+        if k:
+            hn, hs, hmn, hmx = hn + k, hs + k * x, min(hmn, x), max(hmx, x)
+
+    for f in freqs:
+        if f > 16:
+            heavy(1, f)
+        else:
+            cnt[f] += 1
+    wpl, p, pm = 0, 0, 0
+    for w in range(1, 17):
+        c = cnt[w] + ((pm >> w) & 1)
+        if p and c:
+            wpl += p + w
+            pm |= 1 << (p + w)
+            c -= 1
+            p = 0
+        pairs = c >> 1
+        wpl += pairs * 2 * w
+        if 2 * w <= 16:
+            cnt[2 * w] += pairs
+        else:
+            heavy(pairs, 2 * w)
+        if c & 1:
+            p = w
+    for b in range(17, 32):
+        heavy((pm >> b) & 1, b)
+    assert hn <= 3, hn
+    h1, h3 = hmn, hmx
+    h2 = hs - h1 - h3 if hn == 3 else h3
+    if p:
+        if hn == 3:
+            s = p + h1
+            wpl += 2 * s + 2 * h2 + h3 + min(s, h3)
+        elif hn == 2:
+            wpl += 2 * (p + h1) + h2
+        elif hn == 1:
+            wpl += p + h1
+    else:
+        if hn == 3:
+            wpl += 2 * (h1 + h2) + h3
+        elif hn == 2:
+            wpl += h1 + h3
+    return wpl
+
+
+def test_huffman_register_merge_model_is_exact():
+    """The narrow path's register merge (16 weight buckets + <= 3 heavy nodes + a final
+    merge of <= 4 nodes) gives the reference heap's size on every golden block and on
+    random frequency multisets of every shape a block can hold (<= 65 symbols): many
+    light leaves, heavy leaves (17..64), and mixes whose pending merges reach every bucket."""
+    g = _huffman_golden()
+
+    def bits(block):
+        c = np.asarray(block).ravel()
+        vals = [int(v) for v in c if v != 0] + ([0] if c[63] == 0 else [])
+        _, f = np.unique(vals, return_counts=True)
+        return 8 * len(vals) + register_merge_wpl([int(x) for x in f])
+
+    for name, b in g["blocks"].items():
+        assert bits(b["coeffs"]) == b["bits"], name
+    rng = np.random.default_rng(1234)
+    for k in range(4000):
+        dens = rng.random()
+        amp = int(rng.choice([1, 2, 3, 5, 8, 16, 31, 100]))
+        blk = rng.integers(-amp, amp + 1, 64) * (rng.random(64) < dens)
+        assert bits(blk) == O.huffman_bits(blk), blk.tolist()
+    # frequency multisets straight from a partition of up to 64 symbols (distinct nonzero values;
+    # c[63] nonzero, so no extra zero symbol): heavy leaves (17..64) and light ones in every mix
+    for k in range(4000):
+        left, f = int(rng.integers(1, 65)), []
+        while left:
+            x = int(min(left, rng.choice([1, 1, 2, 3, 4, int(rng.integers(1, 65))])))
+            f.append(x)
+            left -= x
+        blk = np.array([v + 1 for v, x in enumerate(f) for _ in range(x)] + [0] * 64)[:64]
+        blk = np.roll(blk, 64 - sum(f))  # nonzeros last: c[63] != 0
+        assert 8 * sum(f) + register_merge_wpl(f) == O.huffman_bits(blk), f
+
+
 def test_legacy_tables_golden():
     """The oracle's explicit-table transforms reproduce the reference's outputs for
     block sizes above 64 and for caller-edited public tables (tests/golden/
