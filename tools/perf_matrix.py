@@ -1,7 +1,9 @@
 """Forward DCT+quant over the bench's step (64 4K luma + 128 1080p chroma planes, one
 multi-plane launch) for every input kind x plan, each next to the no-arithmetic
 movement of the same planes (dctq_diag_movement_planes) on the same box:
-HIP events, interleaved, medians.  Prints one line per configuration.
+HIP events, medians of samples of 3 launches back to back after one untimed
+launch of the same kind (steady state: profiles/r02/policy_b2b.md).  Prints one
+line per configuration.
 
     python tools/perf_matrix.py [frames]
 """
@@ -22,16 +24,18 @@ oc = torch.empty((nc, 64), dtype=torch.int16, device="cuda")
 fb = torch.zeros(1, dtype=torch.int64, device="cuda")
 
 
-def timed(fn, reps=10):
+def timed(fn, reps=8, b2b=3):
     ts = []
     for r in range(reps + 1):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
         fn()
+        e0.record()
+        for _ in range(b2b):
+            fn()
         e1.record()
         torch.cuda.synchronize()
         if r:
-            ts.append(e0.elapsed_time(e1) * 1e-3)
+            ts.append(e0.elapsed_time(e1) * 1e-3 / b2b)
     return statistics.median(ts)
 
 
@@ -40,7 +44,7 @@ print(f"{'kind':8s} {'plan':8s} {'forward us':>10s} {'% 8TB/s':>8s} {'ceiling us
 for kind in ("uniform", "smooth", "const", "extreme"):
     y = dct_amd.synth(12345, kind, 3840, 2160, F)
     c = dct_amd.synth(62345, kind, 1920, 1080, 2 * F)
-    for q, ad in ((50, 0), (90, 0), (50, 1), (10, 0)):
+    for q, ad in ((50, 0), (90, 0), (50, 1), (10, 0), (100, 0)):
         plan = dct_amd.Plan(q, ad, diagnostic=True)
         fb.zero_()
         plan.set_fallback_counter(fb)
