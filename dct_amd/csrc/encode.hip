@@ -35,6 +35,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
                                                                    uint32_t *__restrict__ tiles) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
     __shared__ ExactTables tab;
+    __shared__ uint16_t scr[kWaves * 64];  // resolve_ties_compact's entries
     load_exact_tables(&tab, dev);
     const PlaneSet &ps = es.ps;
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, false>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)nblk, vn, mlo, mhi);
         fence_rows(nxt);  // the prefetch wait: retires the previous batch's stores too
-        resolve_ties<ADAPTIVE>(&tab, cur, stage, lane, wv, mlo, mhi);
+        resolve_ties_compact<ADAPTIVE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         wave_sync();
         u4v q[8];
         stage_chunks(stage, wv, lane, q);

@@ -265,10 +265,17 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
 }
 
+#ifndef DCTQ_INSTAGE_LANES
+// A batch with at least this many flagged blocks resolves its ties in the stage,
+// before its stores (resolve_in_stage); sparser batches queue them.  65 = never.
+#define DCTQ_INSTAGE_LANES 8
+#endif
+
 // One 64-block batch of the v2 loop.  `nxt` holds this batch's rows on entry and
 // the next batch's rows on exit.
 template <bool ADAPTIVE, bool VAR, bool STATS>
 __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables *__restrict__ dev,
+                                            const ExactTables *tab,
                                             unsigned long long *fallbacks, uint4 *stage, uint32_t *qb, uint16_t *qc,
                                             uint4 *ring, int &qn, uint2 (&nxt)[8], uint32_t g, uint32_t step, int lane,
                                             int wv) {
@@ -312,6 +319,15 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
         else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
     }
 
+    if (!valid || (DCTQ_ABLATE & 8)) mlo = mhi = 0;
+    if (DCTQ_INSTAGE_LANES <= 64 &&
+        __builtin_popcountll(__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) >= DCTQ_INSTAGE_LANES)
+    {
+        // tie-heavy batch: resolved in the stage before its stores (no stash, no patches)
+        const uint32_t n = resolve_ties_compact<ADAPTIVE>(tab, cur, stage, qc + qn, lane, wv, mlo, mhi);
+        if (STATS && n) atomicAdd(fallbacks, (unsigned long long)n);
+    }
+
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -351,7 +367,6 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     }
 
     // ---- defer flagged coefficients to the wave's queue (rare: ~1.5 per batch at q50)
-    if (!valid || (DCTQ_ABLATE & 8)) mlo = mhi = 0;
     if (DCTQ_ABLATE & 32) asm volatile("" : "+v"(mlo), "+v"(mhi), "+s"(qn));  // keep code, never run (diagnostic)
     uint64_t has = __builtin_amdgcn_ballot_w64((DCTQ_ABLATE & 32) ? (mlo == 0x12345u && mhi == 0x6789u) : (mlo | mhi) != 0);
     const int16_t *mine16 = reinterpret_cast<const int16_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 2);
@@ -394,6 +409,8 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneSet ps, FastT
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
     __shared__ uint32_t qblk[kWaves * kQCap];
     __shared__ uint16_t qcoef[kWaves * kQCap];
+    __shared__ ExactTables tab;  // the in-stage resolution's D and Q (1 KiB; 4 workgroups still fit a CU)
+    load_exact_tables(&tab, dev);
     // readfirstlane: the wave index is uniform, so batch pointers and buffer
     // descriptors live in SGPRs (no waterfall loops around the stores)
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -414,7 +431,7 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneSet ps, FastT
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
     for (; g < nbatch; g += step)
-        fdct8_batch<ADAPTIVE, VAR, STATS>(ps, dev, fallbacks, stage, qb, qc, ring, qn, nxt, g, step, lane, wv);
+        fdct8_batch<ADAPTIVE, VAR, STATS>(ps, dev, &tab, fallbacks, stage, qb, qc, ring, qn, nxt, g, step, lane, wv);
     if (DCTQ_ABLATE & 16) qn = 0;
     if (DCTQ_ABLATE & 2048) qn = 0;  // diagnostic: skip the final drain
     while (qn > 0) drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
@@ -457,12 +474,12 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 // ============================================================================
 // v3 (small launches): v2's loop with the flagged coefficients resolved IN
 // PLACE (the fused round trip's and the encoder's method, fdct8_core.h
-// resolve_ties) instead of the wave queue: after the prefetch fence, each lane
-// recomputes its own flagged coefficients in the reference's exact order from
-// the pixels still in its registers (tables from a 1 KiB LDS copy) and patches
-// the stage before the 1 KiB stores.  No stash, no drains, no patch stores.
-// On streams it is slower than v2 (divergent fp64 passes in ~78 % of batches,
-// DESIGN.md 3.1), but when every wave has at most one batch (a single frame:
+// resolve_ties_compact) instead of the wave queue: after the prefetch fence,
+// the batch's flagged coefficients are recomputed in the reference's exact order
+// from the pixels still in registers, one entry per lane (tables from a 1 KiB LDS
+// copy), into the stage before the 1 KiB stores.  No stash, no drains, no patch
+// stores.  On streams of sparse ties it is slower than v2's queue (an fp64 pass
+// in ~78 % of batches), but when every wave has at most one batch (a single frame:
 // 512x512 = 64 batches, 4K = 2 025) v2's end-of-kernel drain -- vmcnt(0), stash
 // loads, fp64, patch stores -- is the whole tail of the launch.
 template <bool ADAPTIVE, bool VAR, bool STATS>
@@ -470,6 +487,7 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v3(PlaneSet ps, const
                                                               unsigned long long *fallbacks) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
     __shared__ ExactTables tab;
+    __shared__ uint16_t scr[kWaves * 64];  // resolve_ties_compact's entries
     load_exact_tables(&tab, dev);
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nbatch = ps.first[ps.n];
@@ -495,7 +513,7 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v3(PlaneSet ps, const
         // the prefetch wait (retires the previous batch's stores too), then LDS reads
         asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                      "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-        resolved += resolve_ties<ADAPTIVE>(&tab, cur, stage, lane, wv, mlo, mhi);
+        resolved += resolve_ties_compact<ADAPTIVE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         wave_sync();
         u4v val[8];
         stage_chunks(stage, wv, lane, val);

@@ -334,6 +334,12 @@ __device__ __forceinline__ int pop_flag(uint32_t &mlo, uint32_t &mhi) {
     return (((slot >> 1) & 7) << 3) + ((slot >> 4) << 1) + (slot & 1);
 }
 
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // In-place tie resolution, for consumers that read the final ints from the
 // stage in the same launch (the fused round trip and the encoder).  The exact
 // path's tables live in LDS (one 1 KiB copy per workgroup): per-lane global
@@ -401,30 +407,51 @@ __device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict_
     if (!valid) mlo = mhi = 0;
 }
 
-// Phase 2 (after the prefetch fence): each owning lane recomputes its flagged
-// coefficients in the reference's exact order from the pixels still in its
-// registers and patches the stage.  Returns the lane's recomputation count.
+// Phase 2 (after the prefetch fence): the batch's flagged coefficients resolved
+// in place, compacted: every flagged (block, coefficient) becomes one entry, up
+// to 64 entries per pass, one per lane (every lane busy; a loop in which each
+// lane recomputes its own flags ran as many divergent fp64 passes as the busiest
+// lane had flags).  The entry's lane fetches the block's pixel rows from the owning
+// lane's registers (ds_bpermute: no LDS storage), computes the reference-order
+// value (tables in LDS) and writes it into the stage.  `scr` = 64 uint16 of the
+// wave's LDS (entry = coefficient | block lane << 6).  Call after the prefetch
+// fence.  Returns the entries this lane resolved.
 template <bool ADAPTIVE>
-__device__ __forceinline__ uint32_t resolve_ties(const ExactTables *tab, const uint2 (&cur)[8], uint4 *stage,
-                                                 int lane, int wv, uint32_t mlo, uint32_t mhi) {
-    uint32_t n = 0;
-    if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) {
-        int16_t *mine16 = reinterpret_cast<int16_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 2);
-        while (mlo | mhi) {
-            const int c = pop_flag(mlo, mhi);
-            // opaque copy: hoisted out of this loop, the 64 fp64 pixel conversions
-            // would be 128 live VGPRs (and spill the whole kernel)
-            uint2 rows[8];
-#pragma unroll
-            for (int r = 0; r < 8; ++r) {
-                rows[r] = cur[r];
-                asm volatile("" : "+v"(rows[r].x), "+v"(rows[r].y));
+__device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab, const uint2 (&cur)[8], uint4 *stage,
+                                                         uint16_t *scr, int lane, int wv, uint32_t &mlo,
+                                                         uint32_t &mhi) {
+    int16_t *st16 = reinterpret_cast<int16_t *>(stage) + wv * 64 * (kPitch2 / 2);
+    uint32_t mine = 0;
+    uint64_t has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
+    while (has) {
+        uint32_t e = 0;  // entries of this pass
+        while (has && e + (uint32_t)__builtin_popcountll(has) <= 64u) {
+            if (mlo | mhi) {
+                const int c = pop_flag(mlo, mhi);
+                const uint32_t pos =
+                    e + __builtin_amdgcn_mbcnt_hi((uint32_t)(has >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)has, 0u));
+                scr[pos] = (uint16_t)((uint32_t)c | ((uint32_t)lane << 6));
             }
-            mine16[c] = (int16_t)exact_from_rows_lds<ADAPTIVE>(rows, c, tab);
-            ++n;
+            e += (uint32_t)__builtin_popcountll(has);
+            has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
         }
+        wave_sync();
+        const uint32_t ent = (uint32_t)lane < e ? (uint32_t)scr[lane] : 0u;
+        const int src = (int)(ent >> 6);
+        uint2 rows[8];  // the block's rows, from its owning lane (every lane takes part)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            rows[r].x = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)cur[r].x);
+            rows[r].y = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)cur[r].y);
+        }
+        if ((uint32_t)lane < e) {
+            const int c = (int)(ent & 63u);
+            st16[src * (kPitch2 / 2) + c] = (int16_t)exact_from_rows_lds<ADAPTIVE>(rows, c, tab);
+            ++mine;
+        }
+        wave_sync();  // the next pass rewrites scr
     }
-    return n;
+    return mine;
 }
 
 // The wave's stage as the 8 chunks of 1 KiB stores: chunk c, lane l = 16 B at
@@ -438,12 +465,6 @@ __device__ __forceinline__ void stage_chunks(const uint4 *stage, int wv, int lan
         const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
         val[c] = u4v{lo.x, lo.y, hi.x, hi.y};
     }
-}
-
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // vmcnt(0): the wave's stores have read their data VGPRs (and left the CU).

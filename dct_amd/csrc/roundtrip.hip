@@ -95,6 +95,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
                                                           unsigned long long *fallbacks) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
     __shared__ ExactTables tab;
+    __shared__ uint16_t scr[kWaves * 64];  // resolve_ties_compact's entries
     load_exact_tables(&tab, dev);
     const PlaneSet &ps = rt.ps;
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
         retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
-        const uint32_t ne = resolve_ties<ADAPTIVE>(&tab, cur, stage, lane, wv, mlo, mhi);
+        const uint32_t ne = resolve_ties_compact<ADAPTIVE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
         wave_sync();
 
