@@ -86,6 +86,9 @@ def parse():
                          "~25 ms of load to ramp: profiles/r02/clock_ramp.md)")
     ap.add_argument("--per-plane", action="store_true",
                     help="two launches per step (luma, then chroma) instead of one multi-plane launch")
+    ap.add_argument("--dist-legs", action="store_true",
+                    help="at one process: form a one-rank process group (--backend) and run the N>1 legs anyway "
+                         "(gather, band, symbol-stream gather): the RCCL code path on a single GPU")
     ap.add_argument("--backend", default="nccl", help="N>1 process group (nccl = RCCL; gloo only to rehearse "
                                                       "several ranks on one GPU)")
     return ap.parse_args()
@@ -363,7 +366,7 @@ def encode_leg(args, plan, luma, chroma, world, dev):
     def timed(fn):
         fn()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -371,7 +374,7 @@ def encode_leg(args, plan, luma, chroma, world, dev):
             fn()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        if world > 1:
+        if dist.is_initialized():
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -399,7 +402,7 @@ def encode_leg(args, plan, luma, chroma, world, dev):
                       "blocks_per_s": world * n * args.encode_steps / el_h,
                       "ms_per_step": el_h / args.encode_steps * 1e3, "bits_per_block": mean_bits,
                       "compression_vs_u8": 512.0 / mean_bits, "_check": huf_check}
-    if world > 1:
+    if dist.is_initialized():
         def encode_gather():
             encode()
             return shard.gather_symbols(off, sym)
@@ -439,7 +442,7 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
     def timed(fn):
         fn()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -447,7 +450,7 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
             fn()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        if world > 1:
+        if dist.is_initialized():
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -586,7 +589,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # --dist-legs at one process: a one-rank process group over the chosen backend,
+    # so the N>1 legs (RCCL all-gathers of coefficients and symbol streams, the band
+    # split) run end to end on a single GPU (tests/test_gpu_parity.py)
+    dist_on = world > 1 or args.dist_legs
+    if dist_on and world == 1:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(sk.getsockname()[1]))
+        sk.close()
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if dist_on:
         local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share a GPU
         torch.cuda.set_device(local)
         if args.backend == "nccl":
@@ -595,7 +611,7 @@ def main():
             dist.init_process_group(args.backend)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
-    if world > 1:
+    if dist_on:
         world = dist.get_world_size()  # echo the process group's size, not only the launcher's env
     F = args.frames
     seed = args.seed + 100000 * rank
@@ -641,7 +657,7 @@ def main():
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -649,7 +665,7 @@ def main():
         step(evs[k])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         dist.barrier()
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -673,7 +689,7 @@ def main():
                 if args.ceiling_rounds > 0 and not args.per_plane else None)
 
     gather = band = None
-    if world > 1 and args.gather_steps > 0:
+    if dist_on and args.gather_steps > 0:
         gather = gather_leg(args, plan, world, rank, dev)
         band = band_leg(args, plan, luma, chroma, world, dev)
 
@@ -730,7 +746,7 @@ def main():
                     "reference-order recomputation for guard-band (tie) coefficients",
         }
         print(json.dumps(out))
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -65,7 +65,8 @@ def gather_coefficients(local, counts, group=None):
         send = local.contiguous()
     if dist.get_backend(group) == "nccl":
         out = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(out, send, group=group)
+        # RCCL has no int16 type: the same bytes as int32 (64 coefficients = 32 words a block)
+        dist.all_gather_into_tensor(out.view(torch.int32), send.view(torch.int32), group=group)
         if all(c == m for c in counts):
             return out
         parts = list(out.split(m))

@@ -254,12 +254,19 @@ def test_forced_kernels_adversarial_and_counter(T, dm, variant):
 def test_mid_size_tie_heavy_stream(T, dm):
     """More than 4096 64-block batches (the product dispatch then runs the v2 queue
     kernel, not v3) of tie-heavy content: step blocks (a quarter of the DCs are
-    exact ties) and 0/255 extremes, several qualities, both modes."""
+    exact ties), 0/255 extremes and a plane whose batches alternate between step
+    blocks and uniform noise (both of v2's tie paths in one launch), several
+    qualities, both modes."""
     import oracle as O
     rng = np.random.default_rng(31)
     step = _step_blocks(rng, 270, 1024)  # 276 480 blocks = 4320 batches
     ext = O.synth_plane(5, O.KINDS["extreme"], 8 * 1024, 8 * 270)
-    for px in (step, ext):
+    # batches alternating between tie-heavy (step blocks: resolved in the stage before
+    # the stores) and tie-sparse (uniform noise: the queue, stash and patches) in one launch
+    uni = O.synth_plane(6, O.KINDS["uniform"], 8 * 1024, 8 * 270)
+    heavy = (np.arange(8 * 1024) // 512) % 2 == 0
+    mixed = np.ascontiguousarray(np.where(heavy[None, :], step, uni))
+    for px in (step, ext, mixed):
         g = gpu_px(T, px)
         for q, ad in [(50, 0), (10, 1), (90, 0), (100, 1)]:
             plan = dm.Plan(q, ad)
@@ -270,6 +277,29 @@ def test_mid_size_tie_heavy_stream(T, dm):
             assert np.array_equal(got, O.forward_plane(px, q, ad, 16)), (q, ad)
             if q == 50 and px is step:
                 assert int(cnt.item()) > 1000
+
+
+def test_dist_legs_rccl_one_rank(T, dm):
+    """The N>1 legs of bench.py over a real RCCL process group: one rank on this GPU
+    (bench.py --dist-legs).  The gather leg (BASELINE configs[3]: all_gather_into_tensor
+    of the coefficient planes), the band split of one 4K 4:2:0 frame (three gathers,
+    checked against an unsharded forward) and the encoder's symbol-stream gather run
+    end to end through the nccl backend, in a child process with a time limit."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "bench.py", "--dist-legs", "--steps", "2", "--warmup", "1", "--no-cpu", "--frames", "2",
+           "--total-frames", "2", "--gather-steps", "2", "--round-trip-steps", "0", "--encode-steps", "1",
+           "--ceiling-rounds", "0", "--prewarm-ms", "0"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["config"]["world_size"] == 1 and d["n_gpus"] == 1
+    g, b, e = d["gather"], d["band"], d["encode"]
+    assert "RCCL" in g["op"] and g["own_slice_intact"] and g["world_size"] == 1, g
+    assert "RCCL" in b["op"] and b["gathered_equals_unsharded"], b
+    assert "RCCL" in e["gather_op"] and e["gather_blocks_per_s"] > 0, e
 
 
 def test_diag_stream_moves_bytes(T, dm):
