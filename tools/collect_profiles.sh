@@ -4,14 +4,14 @@
 # afterwards).  Each GPU step has its own time limit; any failure ends the run.
 #   1. separate --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py -> traffic.json
 #      (configuration + library hash recorded: bench.py uses it only for a matching run)
-#   2. rocprofv3 --kernel-trace --stats over the same bench command
+#   2. rocprofv3 --kernel-trace --stats over the bench command (with its clock pre-warm)
 #   3. bench.py (the driver's command), which picks traffic.json up
 #   4. kernel stats of the round trip, RLE and Huffman kernels (tools/rt_bench.py, aux_bench.py)
 set -eu
 export TMPDIR=/tmp
 O=gpurun_out/prof_final
 mkdir -p $O
-B="python bench.py --steps 3 --warmup 1 --no-cpu --round-trip-steps 0 --encode-steps 0 --ceiling-rounds 0"
+B="python bench.py --steps 3 --warmup 1 --no-cpu --round-trip-steps 0 --encode-steps 0 --ceiling-rounds 0 --prewarm-ms 0"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- $B > $O/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o run --output-format csv -- $B > $O/pmc_write.log 2>&1
 python tools/pmc_traffic.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_write/run_counter_collection.csv \
