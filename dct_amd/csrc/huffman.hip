@@ -41,15 +41,20 @@
 #include "dctq_internal.h"
 
 #ifndef DCTQ_HUF_ABLATE
-#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge
+#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge, 4 leaf adds into scrambled rows, 5 no leaf adds
 #endif
 
 namespace dctq {
 
 constexpr int kHufWaves = 4;
 constexpr int kHufThreads = 64 * kHufWaves;
-constexpr int kHufPitch = 144;  // bytes per block in the tile stage (128 + 16: ds_read_b128 spread)
-constexpr int kHufWaveLds = 64 * kHufPitch;  // the tile stage, reused for the histogram (kHistBytes)
+// The wave's tile stage: 64 blocks x 128 B, 16-B piece k of block b at
+// b * 128 + 16 * (k ^ ((b >> 1) & 7)) -- the XOR swizzle makes the lane-per-block
+// ds_read_b128 of tile_row conflict-free (each 16-lane group of a b128 read
+// covers 16 distinct 16-B bank groups) with no padding, so the tile can arrive
+// by LDS-DMA (1 KiB contiguous per instruction; each lane picks its source piece).
+// 9 KiB per wave: the dense/sparse paths reuse it for their histogram (kHistBytes).
+constexpr int kHufWaveLds = 9 * 1024;
 // The narrow path's value counters and weight histogram, one region shared by
 // the workgroup's waves: byte  row * 256 + lane * 4 + wave  is wave `wave`'s
 // 8-bit counter `row` of lane `lane` (counts never exceed 64).  Every lane owns
@@ -135,13 +140,52 @@ __device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine,
 // N-network instead of the 64-one.
 // The lane's 64 coefficients from its row of the tile stage, as 32 dwords.
 __device__ __forceinline__ void tile_row(const char *mine, int lane, uint32_t (&d)[32]) {
+    // the row's address, made opaque per call: eight hoisted loop-invariant piece
+    // addresses spilled; recomputed it is one v_xor per piece
+    int row = (lane << 7) | (((lane >> 1) & 7) << 4);
+    asm volatile("" : "+v"(row));
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const uint4 w = *reinterpret_cast<const uint4 *>(mine + lane * kHufPitch + k * 16);
+        const uint4 w = *reinterpret_cast<const uint4 *>(mine + (row ^ (k << 4)));
         d[4 * k] = w.x;
         d[4 * k + 1] = w.y;
         d[4 * k + 2] = w.z;
         d[4 * k + 3] = w.w;
+    }
+}
+
+// Tile t (blocks 64t .. 64t + nb - 1) into the wave's stage by LDS-DMA: chunk c
+// (1 KiB of LDS) holds blocks 8c .. 8c + 7, lane l the piece (l & 7) ^ ((b >> 1) & 7)
+// of block b = 8c + (l >> 3) (the swizzle of tile_row).  No VGPRs, no ds_write:
+// the next tile streams in while the narrow path works on this one.  The caller
+// has retired its reads of the stage (lgkmcnt(0)); the data is there after
+// vmcnt(0).  Blocks past the end are zeroed by the loop (the tail tile only).
+__device__ __forceinline__ void tile_dma(const int16_t *coef, long long t, long long nblk, char *mine, int lane) {
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    const long long left = nblk - t * 64;
+    const int nb = left < 64 ? (int)left : 64;
+    const uint64_t a = (uint64_t)(coef + t * 64 * 64);
+    const i4 rs = {(int)(uint32_t)a, (int)((a >> 32) & 0xFFFFu), nb * 128, 0x00020000};  // as make_buffer_rsrc
+    // piece (l & 7) ^ (b >> 1 & 7) of block b = 8c + (l >> 3) sits at byte 1024 c + (base ^ 64 (c & 1))
+    int base = ((lane >> 3) << 7) | (((lane & 7) ^ (lane >> 4)) << 4);
+    asm volatile("" : "+v"(base));  // computed here: eight loop-invariant offsets hoisted out of the loop spilled
+    const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)mine;
+    // Inline asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: LLVM's waitcnt pass
+    // cannot tell an LDS-DMA from the workgroup's other LDS traffic and puts a
+    // vmcnt(0) before the next LDS instruction -- the narrow path's first counter
+    // add would wait for the whole prefetch.  The stage is only read after the
+    // explicit vmcnt(0) at the top of the next tile, and M0 is restored.
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        uint32_t save;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %1\n\t"
+            "buffer_load_dwordx4 %2, %3, 0 offen nt lds\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(save)
+            : "s"(lds + c * 1024), "v"(c * 1024 + (base ^ ((c & 1) << 6))), "s"(rs)
+            : "memory");
     }
 }
 
@@ -180,14 +224,13 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
 
 __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes, uint32_t &lmax) {
     uint32_t a[64];
+    {
+        uint32_t d[32];
+        tile_row(mine, lane, d);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint4 w = *reinterpret_cast<const uint4 *>(mine + lane * kHufPitch + k * 16);
-        const uint32_t d[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            a[8 * k + 2 * h] = (d[h] << 16) - 1u;
-            a[8 * k + 2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
+        for (int h = 0; h < 32; ++h) {
+            a[2 * h] = (d[h] << 16) - 1u;
+            a[2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
         }
     }
     sort_net<64>(a);
@@ -211,10 +254,14 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
 //  4. merge as in the dense path (each lane jumps to its next occupied bucket),
 //     every bucket read AND cleared as it is processed.
 // Returns the symbol count and the WPL.
+template <typename NextTile>
 __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lane, int wv, int32_t vmin, uint32_t span,
-                                            bool last_zero, uint32_t &count, uint32_t &wpl) {
+                                            bool last_zero, uint32_t &count, uint32_t &wpl, NextTile next_tile) {
     uint32_t d[32];
     tile_row(mine, lane, d);
+    // the row is in registers and the stage is free: the next tile streams in meanwhile
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    next_tile();
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     const uint32_t base = (uint32_t)(lane * 4);  // byte 0 of the lane's dword in every row
     const uint32_t sh = 8u * (uint32_t)wv, inc = 1u << sh, keep = ~(0xFFu << sh);  // the wave's byte of it
@@ -262,7 +309,13 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
 #pragma unroll
             for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) {
                 lmax = f[s_] > lmax ? f[s_] : lmax;
+#if DCTQ_HUF_ABLATE == 4  // timing: leaf adds into rows that never repeat back to back (wrong sizes)
+                __hip_atomic_fetch_add(at((f[s_] + s_) & 63), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#elif DCTQ_HUF_ABLATE == 5  // timing: no leaf adds (wrong sizes)
+                asm volatile("" ::"v"(f[s_]));
+#else
                 __hip_atomic_fetch_add(at(f[s_]), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
             }
         }
     }
@@ -365,26 +418,24 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
     for (int i = threadIdx.x; i < kHufCtrBytes / 16; i += kHufThreads) ctr_lds[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     const long long stride = (long long)gridDim.x * kHufWaves;
-    for (long long t = (long long)blockIdx.x * kHufWaves + wv; t < ntiles; t += stride) {
+    long long t = (long long)blockIdx.x * kHufWaves + wv;
+    if (t < ntiles) tile_dma(coef, t, nblk, mine, lane);
+    for (; t < ntiles; t += stride) {
         const long long left = nblk - t * 64;
         const int nb = left < 64 ? (int)left : 64;
-        // ---- tile -> LDS: load k covers blocks 8k..8k+7 (16 B per lane, 1 KiB per load)
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<int16_t *>(coef) + t * 64 * 64, (short)0, nb * 128, 0x00020000);  // past the tail: zeros
-        uint4 q[8];
+        // this tile's DMA has landed, and the previous tile's bits store has left
+        // (one in-order vmcnt) before LDS reads land in VGPRs (the store-data hazard)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        if (nb < 64) {  // the launch's last tile: blocks past the end are empty (every path reads them)
+            if (lane >= nb) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, 2 /* nt */);
-            q[k] = make_uint4(v[0], v[1], v[2], v[3]);
+                for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4 *>(mine + lane * 128 + k * 16) = make_uint4(0, 0, 0, 0);
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
         }
-        // the previous tile's histogram reads are done (lgkmcnt) and its bits store
-        // retired with the loads above (one in-order vmcnt) before LDS is rewritten
-        __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            *reinterpret_cast<uint4 *>(mine + (8 * k + (lane >> 3)) * kHufPitch + (lane & 7) * 16) = q[k];
-        __builtin_amdgcn_wave_barrier();
+        bool dma_issued = false;
         uint32_t nz = 0;
         bool last_zero;     // c[63] == 0: value 0 is a symbol once
         bool narrow = false;  // a dense tile whose every block has its values (zeros included) within 64 integers
@@ -443,7 +494,10 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
         } else
 #endif
         if (narrow) {
-            narrow_tile(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl);  // the zero leaf included
+            dma_issued = true;
+            narrow_tile(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl, [&] {
+                if (t + stride < ntiles) tile_dma(coef, t + stride, nblk, mine, lane);
+            });  // the zero leaf included
         } else {
             if (!__builtin_amdgcn_ballot_w64(nz > 16))
                 sparse_runs<16>(mine, lane, nodes, lmax);
@@ -527,6 +581,11 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
             cur = nxt + carry;
         }
         }
+        }
+        if (!dma_issued) {  // the histogram paths used the stage until now
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): their bucket reads are done
+            __builtin_amdgcn_wave_barrier();
+            if (t + stride < ntiles) tile_dma(coef, t + stride, nblk, mine, lane);
         }
         const __amdgpu_buffer_rsrc_t rb =
             __builtin_amdgcn_make_buffer_rsrc(bits + t * 64, (short)0, nb * 4, 0x00020000);
