@@ -899,6 +899,34 @@ def test_huffman_bits_large_plane(T, dm):
     assert L.dctq_huffman_bits(C.c_void_p(c.data_ptr()), 0, C.c_void_p(out.data_ptr()), None) == 0
 
 
+def test_huffman_bits_tile_sequences(T, dm):
+    """Many tiles per wave (20 011 tiles over the kernel's 8 192-wave grid): consecutive tiles
+    of one wave take every pair of paths (narrow counting with the next tile's LDS-DMA in
+    flight, 16/32-input sorts, the 64-network), and the last tile is ragged.  Every block
+    against the oracle (computed once per distinct base tile)."""
+    import oracle as O
+    rng = np.random.default_rng(77)
+    base = []
+    for kind, q, ad in [("uniform", 50, 0), ("extreme", 10, 0), ("smooth", 90, 1), ("const", 50, 0),
+                        ("uniform", 100, 0), ("smooth", 50, 0), ("extreme", 100, 1), ("uniform", 5, 0)]:
+        plane = O.forward_plane(O.synth_plane(int(rng.integers(1 << 30)), O.KINDS[kind], 8 * 64, 8 * 4), q, ad)
+        base += [plane[64 * k:64 * (k + 1)] for k in range(4)]
+    wide = (rng.integers(-300, 301, (64, 64)) * (rng.random((64, 64)) < 0.8)).astype(np.int16)
+    base.append(wide)  # dense, span >= 64: the sort network
+    mid = np.zeros((64, 64), np.int16)  # 17..32 nonzero coefficients per block: the 32-input sort
+    for r in range(64):
+        k = int(rng.integers(17, 33))
+        mid[r, rng.choice(64, k, replace=False)] = rng.integers(-40, 41, k) | 1
+    base.append(mid)
+    base = np.stack(base)
+    want_base = np.stack([O.huffman_bits_plane(b) for b in base])
+    order = rng.integers(0, len(base), 20011)
+    nblk = 64 * (len(order) - 1) + 37
+    coef = base[order].reshape(-1, 64)[:nblk]
+    got = dm.huffman_bits(T.from_numpy(coef).cuda()).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want_base[order].reshape(-1)[:nblk])
+
+
 def test_encode_planes_fused(T, dm):
     """dctq_encode_planes (forward + zigzag/RLE, the count fused into the forward) equals the
     oracle's run_length_encode of the oracle's quantized planes, blocks numbered plane
