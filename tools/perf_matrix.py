@@ -10,6 +10,7 @@ line per configuration.
 import os
 import statistics
 import sys
+import time
 
 import torch
 
@@ -38,6 +39,18 @@ def timed(fn, reps=8, b2b=3):
             ts.append(e0.elapsed_time(e1) * 1e-3 / b2b)
     return statistics.median(ts)
 
+
+# clock ramp (profiles/r02/clock_ramp.md): an idle box needs ~25 ms of load to leave its low clocks,
+# which the first configuration's samples would otherwise absorb
+_y = dct_amd.synth(1, "uniform", 3840, 2160, F)
+_c = dct_amd.synth(2, "uniform", 1920, 1080, 2 * F)
+_p = dct_amd.Plan(50, 0, diagnostic=True)
+_t = time.perf_counter()
+while time.perf_counter() - _t < 0.3:
+    for _ in range(8):
+        _p.forward_quant_planes([_y, _c], outs=[oy, oc])
+    torch.cuda.synchronize()
+del _y, _c, _p
 
 print(f"{'kind':8s} {'plan':8s} {'forward us':>10s} {'% 8TB/s':>8s} {'ceiling us':>10s} {'% 8TB/s':>8s} "
       f"{'fwd/ceil':>8s} {'ties/blk':>8s}")
