@@ -41,7 +41,7 @@
 #include "dctq_internal.h"
 
 #ifndef DCTQ_HUF_ABLATE
-#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge, 4 leaf adds into scrambled rows, 5 no leaf adds
+#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge
 #endif
 
 namespace dctq {
@@ -285,40 +285,41 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
     count = 64u - zeros + (last_zero ? 1u : 0u);
     // readout: every counter read and cleared, THEN the leaves added (the weight
     // histogram reuses the rows).  Only rows below the wave's largest span hold
-    // counts (q50 noise: 32 of 64), in wave-uniform chunks of 8 rows.
-    uint32_t lmax = 0;
-    uint32_t f[64];
+    // counts (q50 noise: 32 of 64), in wave-uniform chunks of 8 rows.  A counter
+    // is kept as its leaf's address: one v_perm moves the wave's byte of the
+    // returned dword into byte 1 (the row) over the lane's byte 0 -- no extract --
+    // and the largest address gives the largest leaf weight.
+    const uint32_t leaf_sel = 0x0C0C0000u | ((4u + (uint32_t)wv) << 8);
+    uint32_t a[64];
 #pragma unroll
     for (int c8 = 0; c8 < 8; ++c8) {
         if (c8 == 0 || __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8))) {
 #pragma unroll
             for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_)
-                f[s_] = (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+                a[s_] = __builtin_amdgcn_perm(
+                    __hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT), base, leaf_sel);
         } else {
 #pragma unroll
-            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) f[s_] = 0;
+            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) a[s_] = base;
         }
     }
 #if DCTQ_HUF_ABLATE == 1  // timing: count + readout only
-    wpl = f[0] + f[63];
+    wpl = a[0] + a[63];
     return;
 #endif
+    uint32_t amax = base;
 #pragma unroll
     for (int c8 = 0; c8 < 8; ++c8) {
         if (c8 == 0 || __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8))) {
 #pragma unroll
             for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) {
-                lmax = f[s_] > lmax ? f[s_] : lmax;
-#if DCTQ_HUF_ABLATE == 4  // timing: leaf adds into rows that never repeat back to back (wrong sizes)
-                __hip_atomic_fetch_add(at((f[s_] + s_) & 63), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#elif DCTQ_HUF_ABLATE == 5  // timing: no leaf adds (wrong sizes)
-                asm volatile("" ::"v"(f[s_]));
-#else
-                __hip_atomic_fetch_add(at(f[s_]), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#endif
+                amax = a[s_] > amax ? a[s_] : amax;
+                __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(ctr + a[s_]), inc, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WAVEFRONT);
             }
         }
     }
+    const uint32_t lmax = amax >> 8;  // the largest leaf weight
 #if DCTQ_HUF_ABLATE == 2  // timing: leaf adds, then a plain clear instead of the merge
 #pragma unroll
     for (int s_ = 0; s_ < 65; ++s_) wpl += (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
