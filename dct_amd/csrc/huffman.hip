@@ -599,8 +599,11 @@ hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bi
     long long grid = (ntiles + kHufWaves - 1) / kHufWaves;
     const long long cap = (long long)num_cus * 8;  // 3 resident per CU (LDS-bound); the rest queue behind them
     if (grid > cap) grid = cap;
-    hipLaunchKernelGGL(huffman_bits_kernel, dim3((unsigned)grid), dim3(kHufThreads), 0, stream, coef, nblk, bits,
-                       ntiles);
+#ifndef DCTQ_HUF_LDS_PAD
+#define DCTQ_HUF_LDS_PAD 0  // A/B: dynamic LDS padding, fewer workgroups per CU (occupancy sensitivity)
+#endif
+    hipLaunchKernelGGL(huffman_bits_kernel, dim3((unsigned)grid), dim3(kHufThreads), DCTQ_HUF_LDS_PAD, stream, coef,
+                       nblk, bits, ntiles);
     return hipGetLastError();
 }
 }  // namespace dctq
