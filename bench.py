@@ -105,6 +105,27 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def gpu_identity():
+    """The box's GPU as rocm-smi reports it (serial, HBM vendor, memory/compute partition):
+    boxes of this pool differ by up to ~15 % on the same bytes, and the
+    bench's own ceilings are the normaliser; this says which box a line came from."""
+    import re
+    import subprocess
+    try:
+        r = subprocess.run(["rocm-smi", "--showserial", "--showmemvendor", "--showmemorypartition",
+                            "--showcomputepartition"], capture_output=True, text=True, timeout=30)
+    except (OSError, subprocess.SubprocessError):
+        return None
+    keys = {"Serial Number": "serial", "GPU memory vendor": "hbm_vendor", "Memory Partition": "memory_partition",
+            "Compute Partition": "compute_partition"}
+    ident = {}
+    for line in r.stdout.splitlines():
+        m = re.match(r"GPU\[0\]\s*:\s*([^:]+?):\s*(\S+)", line)
+        if m and m.group(1).strip() in keys:
+            ident[keys[m.group(1).strip()]] = m.group(2)
+    return ident or None
+
+
 def cpu_share():
     """CPUs this process may use: the cgroup CPU quota if one is set, else the
     scheduler affinity mask; capped by OMP_NUM_THREADS when the environment
@@ -741,6 +762,7 @@ def main():
             "round_trip": round_trip,
             "encode": encode,
             "small_frame": small,
+            "gpu": gpu_identity(),
             "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
                     "reference-order recomputation for guard-band (tie) coefficients",
         }
