@@ -150,18 +150,22 @@ int main(int argc, char **argv) {
         {"rows8  staged  nt", MX(1, 1, 2)}, {"rows8  staged  plain", MX(1, 1, 0)},
         {"rows16 staged  nt", MX(2, 1, 2)}, {"rows16 staged  plain", MX(2, 1, 0)},
     };
-    for (auto &it : items) it.fn();
+    // steady state (profiles/r02/clock_ramp.md, policy_b2b.md): ~300 launches of clock pre-warm, then
+    // per sample one untimed launch of the same case followed by B2B timed launches back to back
+    const int B2B = argc > 2 ? atoi(argv[2]) : 1;
+    for (int w = 0; w < (B2B > 1 ? 300 : 1); ++w) items[w % items.size()].fn();
     CHECK(hipDeviceSynchronize());
     std::vector<std::vector<float>> ms(items.size());
     for (int r = 0; r < reps; ++r)
         for (size_t i = 0; i < items.size(); ++i) {
+            if (B2B > 1) items[i].fn();
             CHECK(hipEventRecord(e0));
-            items[i].fn();
+            for (int k = 0; k < B2B; ++k) items[i].fn();
             CHECK(hipEventRecord(e1));
             CHECK(hipEventSynchronize(e1));
             float t;
             CHECK(hipEventElapsedTime(&t, e0, e1));
-            ms[i].push_back(t);
+            ms[i].push_back(t / B2B);
         }
     CHECK(hipGetLastError());
     for (size_t i = 0; i < items.size(); ++i) {
