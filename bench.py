@@ -221,8 +221,8 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
     planes) partitioned across the ranks in block-row bands
     (dct_amd.shard.band_shard), forward DCT+quant of every band in one
     multi-plane launch, then the coefficient planes all-gathered so every rank
-    holds the whole frame's coefficients (three collectives, ragged bands
-    padded).  Latency-bound (194 400 blocks per frame); max-over-ranks wall
+    holds the whole frame's coefficients (one collective for the three planes,
+    shard.gather_planes; ragged bands padded).  Latency-bound (194 400 blocks per frame); max-over-ranks wall
     time per frame, and a check of the gathered planes against an unsharded
     forward on this rank."""
     from dct_amd import shard
@@ -240,7 +240,7 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
 
     def once():
         plan.forward_quant_planes(bands, outs=outs)
-        return [shard.gather_coefficients(o, c) for o, c in zip(outs, counts)]
+        return shard.gather_planes(outs, counts)  # the three planes in one collective
 
     full = once()
     torch.cuda.synchronize()

@@ -10,9 +10,10 @@ src/quantization.c:113-131), so the path partitions with no data exchange:
 
 The only collectives are OPTIONAL gathers: of the int16 coefficient planes
 (BASELINE configs[3]: "RCCL allgather of quantized coefficient planes over
-xGMI"), or of the run-length symbol streams the encoder makes of them (SURVEY
-8(f)3: shrink the bytes before the exchange).  Each is one all_gather per call
-over the whole shard, padded to the largest shard so ragged splits work.  The
+xGMI"; several planes of a frame in one message with gather_planes), or of the
+run-length symbol streams the encoder makes of them (shrink the
+bytes before the exchange).  Each is one all_gather per call over the whole
+shard, padded to the largest shard so ragged splits work.  The
 ordering of the gathered result equals the unsharded raster order, so rank r's
 slice lands at blocks_before(r).
 """
@@ -78,6 +79,48 @@ def gather_coefficients(local, counts, group=None):
     if all(c == m for c in counts):
         return torch.cat(parts)
     return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+
+def gather_planes(locals_, counts, group=None):
+    """All-gather the coefficient shards of SEVERAL planes (e.g. a frame's Y, Cb
+    and Cr bands: locals_[p] is [counts[p][rank], 64]) in ONE collective: every
+    plane's shard padded to its largest rank, concatenated, exchanged, and split
+    back into per-plane [sum(counts[p]), 64] tensors in rank order.  One message
+    instead of one per plane: each collective pays the RCCL launch and ring
+    latency, and a 4K frame's band is only ~2-4 MB per rank at N = 8."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if len(locals_) != len(counts) or not locals_:
+        raise ValueError("one counts list per plane")
+    for loc, c in zip(locals_, counts):
+        if len(c) != world or loc.shape[0] != c[rank]:
+            raise ValueError("counts must list every rank's shard size of every plane")
+    ms = [max(c) for c in counts]
+    ref = locals_[0]
+    pieces = []
+    for loc, m in zip(locals_, ms):
+        pieces.append(loc.contiguous())
+        if loc.shape[0] < m:
+            pieces.append(torch.zeros((m - loc.shape[0],) + tuple(ref.shape[1:]), dtype=ref.dtype, device=ref.device))
+    send = torch.cat(pieces) if len(pieces) > 1 else pieces[0]
+    M = sum(ms)
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world * M,) + tuple(ref.shape[1:]), dtype=ref.dtype, device=ref.device)
+        # RCCL has no int16 type: the same bytes as int32
+        dist.all_gather_into_tensor(out.view(torch.int32), send.view(torch.int32), group=group)
+        parts = list(out.split(M))
+    else:  # gloo (CPU tests): raw bytes
+        raw = send.view(torch.uint8)
+        parts = [torch.empty_like(raw) for _ in range(world)]
+        dist.all_gather(parts, raw, group=group)
+        parts = [pp.view(ref.dtype) for pp in parts]
+    full, off = [], 0
+    for c, m in zip(counts, ms):
+        full.append(torch.cat([pp[off:off + cr] for pp, cr in zip(parts, c)]))
+        off += m
+    return full
 
 
 def _all_gather_padded(send, m, group):

@@ -50,6 +50,20 @@ def _worker(rank, world, port, q):
         full = shard.gather_coefficients(local, counts)
         assert np.array_equal(full.numpy(), O.forward_plane(plane.numpy(), 90, 1)), "band-sharded gather differs"
 
+        # (2b) a frame's three planes in block-row bands, gathered in ONE collective (bench's band leg)
+        planes = [O.synth_plane(500 + k, O.KINDS[kind], w, h)
+                  for k, (kind, w, h) in enumerate([("uniform", 64, 56), ("smooth", 32, 24), ("extreme", 32, 24)])]
+        locs, cnts = [], []
+        for pl in planes:
+            band, (row0, rows) = shard.band_shard(torch.from_numpy(pl), world, rank)
+            locs.append(torch.from_numpy(O.forward_plane(np.ascontiguousarray(band.numpy()), 50, 0)
+                                         if rows else np.zeros((0, 64), np.int16)))
+            bh = pl.shape[0] // 8
+            cnts.append([(b - a) * (pl.shape[1] // 8) for a, b in (shard.split(bh, world, r) for r in range(world))])
+        fulls = shard.gather_planes(locs, cnts)
+        for pl, f in zip(planes, fulls):
+            assert np.array_equal(f.numpy(), O.forward_plane(pl, 50, 0)), "multi-plane band gather differs"
+
         # (3) run-length streams of the frame shards (what dctq_encode_planes makes on each GPU)
         mine, (lo, hi) = shard.frame_shard(frames, world, rank)
         local = (np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in mine])
