@@ -282,8 +282,8 @@ def test_mid_size_tie_heavy_stream(T, dm):
 def test_dist_legs_rccl_one_rank(T, dm):
     """The N>1 legs of bench.py over a real RCCL process group: one rank on this GPU
     (bench.py --dist-legs).  The gather leg (BASELINE configs[3]: all_gather_into_tensor
-    of the coefficient planes), the band split of one 4K 4:2:0 frame (three gathers,
-    checked against an unsharded forward) and the encoder's symbol-stream gather run
+    of the coefficient planes), the band split of one 4K 4:2:0 frame (its three planes
+    in one gather, checked against an unsharded forward) and the encoder's symbol-stream gather run
     end to end through the nccl backend, in a child process with a time limit."""
     import json
     import subprocess
@@ -300,6 +300,40 @@ def test_dist_legs_rccl_one_rank(T, dm):
     assert "RCCL" in g["op"] and g["own_slice_intact"] and g["world_size"] == 1, g
     assert "RCCL" in b["op"] and b["gathered_equals_unsharded"], b
     assert "RCCL" in e["gather_op"] and e["gather_blocks_per_s"] > 0, e
+
+
+def test_bench_json_contract(T, dm):
+    """bench.py's one JSON line carries what the round driver reads (the metric, the
+    whole-job value, the timing fields, config.workload, the roofline object with
+    bound/achieved/peak/unit/frac/traffic, the CPU baseline with value/unit/cores/
+    kind/sample) and its own parity check passes; a short run in a child process."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--frames", "2", "--cpu-seconds", "2",
+           "--ceiling-rounds", "1", "--round-trip-steps", "1", "--encode-steps", "1", "--prewarm-ms", "20"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.strip().splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["warmup"] == 1 and d["higher_is_better"] is True
+    assert d["value"] > 0 and abs(d["value"] * d["ms_per_step"] * 1e-3 - d["config"]["blocks_per_gpu_step"]) < 1e-3 * d["value"]
+    assert "workload" in d["config"]
+    ro = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in ro, k
+    assert ro["bound"] == "hbm" and ro["unit"] == "GB/s" and 0 < ro["frac"] < 1
+    assert abs(ro["frac"] - ro["achieved"] / ro["peak"]) < 1e-9
+    cb = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in cb, k
+    assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] >= 1
+    assert d["parity_check"] is True and d["encode"]["huffman"]["parity_check_chroma0"] is True
 
 
 def test_diag_stream_moves_bytes(T, dm):
