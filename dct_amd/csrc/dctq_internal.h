@@ -35,6 +35,16 @@ inline int resident_per_cu(K kernel, int threads) {
     return nb;
 }
 
+// Persistent grid-stride kernels launch DCTQ_GRID_MULT times their resident
+// workgroups; the extra ones queue and start as the first wave of workgroups
+// retires, which evens out batches of unequal cost and the launch tail
+// (profiles/r02/grid_mult_ab.log: x8 is 2.4-7 % faster than x1 on the forward,
+// round trip, inverse and encoder, outputs identical; x16/x32 regress on
+// uniform input).  The forward's stash ring is sized for this grid.
+#ifndef DCTQ_GRID_MULT
+#define DCTQ_GRID_MULT 8
+#endif
+
 // n / d and n % d by multiply-high, valid for 0 <= n < 2^31 (host-built magic).
 struct FastDiv {
     uint32_t d, m, s;

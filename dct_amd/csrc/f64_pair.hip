@@ -214,7 +214,7 @@ static hipError_t launch_persistent(K kernel, long long nblk, int num_cus, hipSt
     const int per_cu = resident_per_cu(kernel, kThreadsP);
     const long long nbatch = (nblk + 31) / 32;
     const long long want = (nbatch + kWavesP - 1) / kWavesP;
-    const long long cap = (long long)num_cus * per_cu;
+    const long long cap = (long long)num_cus * per_cu * DCTQ_GRID_MULT;
     hipLaunchKernelGGL(kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(kThreadsP), 0, stream, args...);
     return hipGetLastError();
 }

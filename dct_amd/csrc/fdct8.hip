@@ -464,7 +464,7 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
     static const int per_cu = resident_per_cu(fdct8_quant_v2<A, V, S>, kThreads);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    uint32_t cap = (uint32_t)(num_cus * per_cu);
+    uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
     if (cap > (uint32_t)ring_wgs) cap = (uint32_t)ring_wgs;
     hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps, t, dev,
                        fb, (uint4 *)ring);
@@ -551,7 +551,7 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
     const bool a = adaptive != 0, v = ps.var[0] != nullptr, s = fallbacks != nullptr;
     if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
     // at most one batch per wave of the resident grid: in-place ties (no drain tail)
-    const bool single = ps.first[ps.n] <= (uint32_t)ring_wgs * kWaves;
+    const bool single = ps.first[ps.n] <= (uint32_t)(ring_wgs / DCTQ_GRID_MULT) * kWaves;
     if (variant == 3 || (variant == 2 && single))  // variant 4: the queue kernel at any size (A/B)
         DCTQ_SELECT(return launch_v3, a, v, s, (ps, dev, fallbacks, stream, num_cus));
     DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring, ring_wgs));
@@ -624,7 +624,7 @@ hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num
     static const int per_cu = resident_per_cu(fdct8_movement, kThreads);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_v2
     hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps);
     return hipGetLastError();
 }

@@ -190,7 +190,7 @@ static hipError_t launch_rt(const RoundTripSet &rt, const DevTables *dev, unsign
     static const int per_cu = resident_per_cu(roundtrip8<A, V, S>, kThreads);
     const uint32_t nbatch = rt.ps.first[rt.ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
     hipLaunchKernelGGL((roundtrip8<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt, dev, fb);
     return hipGetLastError();
 }
