@@ -136,8 +136,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
         delete p;
         return fail(DCTQ_EHIP, "hipMemcpy(plan tables)", e);
     }
-    // the v2 grid: at most 4 resident 256-thread workgroups per CU (LDS-bound), times DCTQ_GRID_MULT
-    p->ring_wgs = p->num_cus * 4 * DCTQ_GRID_MULT;
+    p->ring_wgs = dctq::fdct8_ring_workgroups(p->num_cus);  // the v2 grid's workgroups
     e = hipMalloc(&p->ring, dctq::fdct8_ring_bytes(p->ring_wgs));
     if (e != hipSuccess) {
         (void)hipFree(p->dev);

@@ -116,6 +116,7 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
                               int ring_wgs);
 // bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
 size_t fdct8_ring_bytes(int workgroups);
+int fdct8_ring_workgroups(int num_cus);
 // diagnostic: fdct8_quant_v2's data movement without arithmetic (fdct8.hip)
 hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num_cus);
 hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,

@@ -402,25 +402,34 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     }
 }
 
+// Waves per workgroup of the stream kernels (v2, v3, movement).  Every wave is
+// independent (own stage slice, queue, stash slot); only the 1 KiB exact-table
+// copy is shared per workgroup.
+#ifndef DCTQ_FWD_WAVES
+#define DCTQ_FWD_WAVES 4
+#endif
+constexpr int kFWaves = DCTQ_FWD_WAVES;
+constexpr int kFThreads = 64 * kFWaves;
+
 template <bool ADAPTIVE, bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v2(PlaneSet ps, FastTables t,
+__global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v2(PlaneSet ps, FastTables t,
                                                               const DevTables *__restrict__ dev,
                                                               unsigned long long *fallbacks, uint4 *ring_all) {
-    __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ uint32_t qblk[kWaves * kQCap];
-    __shared__ uint16_t qcoef[kWaves * kQCap];
+    __shared__ uint4 stage[kFThreads * kPitch2 / 16];
+    __shared__ uint32_t qblk[kFWaves * kQCap];
+    __shared__ uint16_t qcoef[kFWaves * kQCap];
     __shared__ ExactTables tab;  // the in-stage resolution's D and Q (1 KiB; 4 workgroups still fit a CU)
     load_exact_tables(&tab, dev);
     // readfirstlane: the wave index is uniform, so batch pointers and buffer
     // descriptors live in SGPRs (no waterfall loops around the stores)
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t step = gridDim.x * kWaves;
+    const uint32_t step = gridDim.x * kFWaves;
     uint32_t *qb = qblk + wv * kQCap;
     uint16_t *qc = qcoef + wv * kQCap;
-    uint4 *ring = ring_all + (size_t)(blockIdx.x * kWaves + wv) * kQCap * 4;  // 64 B per queue slot
+    uint4 *ring = ring_all + (size_t)(blockIdx.x * kFWaves + wv) * kQCap * 4;  // 64 B per queue slot
     int qn = 0;
-    uint32_t g = blockIdx.x * kWaves + wv;
+    uint32_t g = blockIdx.x * kFWaves + wv;
     uint2 nxt[8];
     {
         const int k0 = plane_of(ps, g);
@@ -461,12 +470,12 @@ static hipError_t launch_v1(const PlaneSet &ps, const FastTables &t, const DevTa
 template <bool A, bool V, bool S>
 static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTables *dev, unsigned long long *fb,
                             hipStream_t stream, int num_cus, void *ring, int ring_wgs) {
-    static const int per_cu = resident_per_cu(fdct8_quant_v2<A, V, S>, kThreads);
+    static const int per_cu = resident_per_cu(fdct8_quant_v2<A, V, S>, kFThreads);
     const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
+    const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
     uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
     if (cap > (uint32_t)ring_wgs) cap = (uint32_t)ring_wgs;
-    hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps, t, dev,
+    hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps, t, dev,
                        fb, (uint4 *)ring);
     return hipGetLastError();
 }
@@ -483,16 +492,16 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 // 512x512 = 64 batches, 4K = 2 025) v2's end-of-kernel drain -- vmcnt(0), stash
 // loads, fp64, patch stores -- is the whole tail of the launch.
 template <bool ADAPTIVE, bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v3(PlaneSet ps, const DevTables *__restrict__ dev,
+__global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, const DevTables *__restrict__ dev,
                                                               unsigned long long *fallbacks) {
-    __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ uint4 stage[kFThreads * kPitch2 / 16];
     __shared__ ExactTables tab;
-    __shared__ uint16_t scr[kWaves * 64];  // resolve_ties_compact's entries
+    __shared__ uint16_t scr[kFWaves * 64];  // resolve_ties_compact's entries
     load_exact_tables(&tab, dev);
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t step = gridDim.x * kWaves;
-    uint32_t g = blockIdx.x * kWaves + wv;
+    const uint32_t step = gridDim.x * kFWaves;
+    uint32_t g = blockIdx.x * kFWaves + wv;
     uint2 nxt[8];
     prefetch_batch(ps, g, lane, nxt);
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
@@ -535,15 +544,18 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_quant_v3(PlaneSet ps, const
 template <bool A, bool V, bool S>
 static hipError_t launch_v3(const PlaneSet &ps, const DevTables *dev, unsigned long long *fb, hipStream_t stream,
                             int num_cus) {
-    static const int per_cu = resident_per_cu(fdct8_quant_v3<A, V, S>, kThreads);
+    static const int per_cu = resident_per_cu(fdct8_quant_v3<A, V, S>, kFThreads);
     const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu);
-    hipLaunchKernelGGL((fdct8_quant_v3<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps, dev, fb);
+    const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
+    hipLaunchKernelGGL((fdct8_quant_v3<A, V, S>), dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps, dev, fb);
     return hipGetLastError();
 }
 
-size_t fdct8_ring_bytes(int workgroups) { return (size_t)workgroups * kWaves * kQCap * 64; }
+size_t fdct8_ring_bytes(int workgroups) { return (size_t)workgroups * kFWaves * kQCap * 64; }
+// Workgroups the stash ring serves: the resident ones (16 waves per CU: 4 per SIMD, VGPR-bound) times the
+// grid multiplier.
+int fdct8_ring_workgroups(int num_cus) { return num_cus * (16 / kFWaves) * DCTQ_GRID_MULT; }
 
 hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
                               unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus, void *ring,
@@ -551,7 +563,7 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
     const bool a = adaptive != 0, v = ps.var[0] != nullptr, s = fallbacks != nullptr;
     if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
     // at most one batch per wave of the resident grid: in-place ties (no drain tail)
-    const bool single = ps.first[ps.n] <= (uint32_t)(ring_wgs / DCTQ_GRID_MULT) * kWaves;
+    const bool single = ps.first[ps.n] <= (uint32_t)(ring_wgs / DCTQ_GRID_MULT) * kFWaves;
     if (variant == 3 || (variant == 2 && single))  // variant 4: the queue kernel at any size (A/B)
         DCTQ_SELECT(return launch_v3, a, v, s, (ps, dev, fallbacks, stream, num_cus));
     DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring, ring_wgs));
@@ -563,15 +575,15 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
 // kernel -- bench.py reports kernel time / this time).  Same persistent grid,
 // occupancy, prefetch, LDS stage, fence and 1 KiB non-temporal stores as
 // fdct8_batch; the "coefficients" are the pixel rows twice over.
-__global__ __launch_bounds__(kThreads, 4) void fdct8_movement(PlaneSet ps) {
-    __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ uint32_t qpad[kWaves * kQCap];   // same LDS footprint as fdct8_quant_v2
-    __shared__ uint16_t qpad2[kWaves * kQCap];  // (occupancy is LDS-bound)
+__global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps) {
+    __shared__ uint4 stage[kFThreads * kPitch2 / 16];
+    __shared__ uint32_t qpad[kFWaves * kQCap];   // same LDS footprint as fdct8_quant_v2
+    __shared__ uint16_t qpad2[kFWaves * kQCap];  // (occupancy is LDS-bound)
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (ps.n < 0) { qpad[threadIdx.x] = 0; qpad2[threadIdx.x] = 0; }  // keep the padding allocated
     const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t step = gridDim.x * kWaves;
-    uint32_t g = blockIdx.x * kWaves + wv;
+    const uint32_t step = gridDim.x * kFWaves;
+    uint32_t g = blockIdx.x * kFWaves + wv;
     uint2 nxt[8];
     {
         const int k0 = plane_of(ps, g);
@@ -621,11 +633,11 @@ __global__ __launch_bounds__(kThreads, 4) void fdct8_movement(PlaneSet ps) {
 }
 
 hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num_cus) {
-    static const int per_cu = resident_per_cu(fdct8_movement, kThreads);
+    static const int per_cu = resident_per_cu(fdct8_movement, kFThreads);
     const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
+    const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
     const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_v2
-    hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, ps);
+    hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps);
     return hipGetLastError();
 }
 }  // namespace dctq

@@ -567,9 +567,13 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
     }
 }
 
-static unsigned grid_for(long long waves_wanted, int num_cus) {
+// Grid = at most per_cu workgroups per CU (far more than are resident: the queued ones refill retiring
+// slots at once, which evens out tiles of unequal symbol counts).  Against 16 per CU, one box
+// (profiles/r02/grid_mult_ab.log, tools/rle_ab.py): count -3 to -5 % at 128, emit -1 to -8 % and decode
+// 0 to -9 % at 64 (128 is one tile per wave at 64 4K frames; it loses 11 % on constant-block decode).
+static unsigned grid_for(long long waves_wanted, int num_cus, int per_cu) {
     long long g = (waves_wanted + kRleWaves - 1) / kRleWaves;
-    const long long cap = (long long)num_cus * 16;
+    const long long cap = (long long)num_cus * per_cu;
     return (unsigned)(g < 1 ? 1 : g > cap ? cap : g);
 }
 
@@ -599,7 +603,7 @@ hipError_t launch_rle_fixup(uint32_t *offsets, long long nblk, const void *ws, l
 hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offsets, void *ws, hipStream_t stream,
                             int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
-    hipLaunchKernelGGL(rle_count_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, coef, nblk,
+    hipLaunchKernelGGL(rle_count_kernel, dim3(grid_for(ntiles, num_cus, 128)), dim3(kRleThreads), 0, stream, coef, nblk,
                        offsets, (uint32_t *)ws, ntiles);
     hipError_t e = launch_rle_scan(ws, ntiles, stream);
     if (e != hipSuccess) return e;
@@ -609,7 +613,7 @@ hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offse
 hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,
                            unsigned long long capacity, hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
-    hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, coef, nblk,
+    hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, coef, nblk,
                        offsets, symbols, ntiles, capacity);
     return hipGetLastError();
 }
@@ -617,7 +621,7 @@ hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *
 hipError_t launch_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblk, int16_t *coef,
                              hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
-    hipLaunchKernelGGL(rle_decode_kernel, dim3(grid_for(ntiles, num_cus)), dim3(kRleThreads), 0, stream, symbols,
+    hipLaunchKernelGGL(rle_decode_kernel, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, symbols,
                        offsets, nblk, coef, ntiles);
     return hipGetLastError();
 }
