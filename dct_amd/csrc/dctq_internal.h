@@ -41,6 +41,13 @@ inline int resident_per_cu(K kernel, int threads) {
 // (profiles/r02/grid_mult_ab.log: x8 is 2.4-7 % faster than x1 on the forward,
 // round trip, inverse and encoder, outputs identical; x16/x32 regress on
 // uniform input).  The forward's stash ring is sized for this grid.
+// Cache policy of the bulk 1 KiB output stores of every streaming kernel
+// (buffer-store aux bits, gfx950: 1 sc0, 2 nt, 16 sc1).  Non-temporal: the
+// written lines are never re-read by the kernel that writes them.
+#ifndef DCTQ_NT_AUX
+#define DCTQ_NT_AUX 2
+#endif
+
 #ifndef DCTQ_GRID_MULT
 #define DCTQ_GRID_MULT 8
 #endif

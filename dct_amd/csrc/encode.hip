@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128, (short)0, nb * 128, 0x00020000);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(q[c], rs, lane * 16, c * 1024, 2 /* nt */);
+            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(q[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
         }
         uint32_t *off = offsets + es.blk_first[k] + (size_t)b * 64;
         uint32_t run = 0;

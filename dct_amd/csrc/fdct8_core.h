@@ -88,7 +88,7 @@ constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) con
 // Non-temporal: -15 % kernel time on the 4K stream (profiles/r01/store_policy.md);
 // the written lines are never re-read by this kernel except by tie patches,
 // which come after a vmcnt(0).
-#define DCTQ_STORE_AUX 2
+#define DCTQ_STORE_AUX DCTQ_NT_AUX
 #endif
 #ifndef DCTQ_LOAD_NT
 #define DCTQ_LOAD_NT 1  // pixel rows are read exactly once

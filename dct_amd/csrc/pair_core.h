@@ -77,7 +77,7 @@ __device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane
         val[k] = u4p{t.x, t.y, t.z, t.w};
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, 2 /* nt */);
+    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
 }
 
 }  // namespace dctq

@@ -562,7 +562,7 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(coef + (b0 + h) * 64, (short)0, (he - h) * 128, 0x00020000);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, 2);
+            for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
         }
     }
 }

@@ -152,11 +152,11 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 reinterpret_cast<char *>(coef) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, 2);
+            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
             if (VAR) {
                 const __amdgpu_buffer_rsrc_t rv =
                     __builtin_amdgcn_make_buffer_rsrc(ps.var[k] + (size_t)b * 64, (short)0, (int)(nb * 4u), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_NT_AUX);
             }
         }
 
