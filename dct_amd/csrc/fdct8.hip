@@ -290,11 +290,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
     const uint32_t n = b * 64 + lane;
     const bool valid = n < (uint32_t)p.nblk;
-    {
-        const uint32_t gn = g + step;  // past the end: the last plane's block 0 (re-read, unused)
-        const int kn = plane_of(ps, gn);
-        load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
-    }
+    prefetch_batch(ps, g + step, lane, nxt);
 
     uint32_t mlo, mhi;
     int32_t var_num;
@@ -598,11 +594,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps) {
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-        {
-            const uint32_t gn = g + step;
-            const int kn = plane_of(ps, gn);
-            load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
-        }
+        prefetch_batch(ps, g + step, lane, nxt);
         uint2 *mine = reinterpret_cast<uint2 *>(reinterpret_cast<char *>(stage) + (wv * 64 + lane) * kPitch2);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {

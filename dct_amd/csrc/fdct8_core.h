@@ -470,8 +470,17 @@ __device__ __forceinline__ void stage_chunks(const uint4 *stage, int wv, int lan
 // vmcnt(0): the wave's stores have read their data VGPRs (and left the CU).
 __device__ __forceinline__ void retire_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
-// Rows of global batch gn (past the end: the last plane's block 0, unused).
+// Rows of global batch gn.  Past the end (a wave's last batch), SKIP loads
+// nothing: the rows would be unused, and with the grid 8x the resident one every
+// wave pays that tail once (forward -0.3 to -7 %, q100 most; the fused round trip
+// measured +1 % and keeps the load of the last plane's block 0:
+// profiles/r02/grid_mult_ab.log).
+#ifndef DCTQ_SKIP_TAIL_PF
+#define DCTQ_SKIP_TAIL_PF 1
+#endif
+template <bool SKIP = true>
 __device__ __forceinline__ void prefetch_batch(const PlaneSet &ps, uint32_t gn, int lane, uint2 (&nxt)[8]) {
+    if (SKIP && DCTQ_SKIP_TAIL_PF && gn >= ps.first[ps.n]) return;  // wave-uniform
     const int kn = plane_of(ps, gn);
     load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
 }

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        if (DCTQ_RT_EARLY_PREFETCH) prefetch_batch(ps, g + step, lane, nxt);
+        if (DCTQ_RT_EARLY_PREFETCH) prefetch_batch<false>(ps, g + step, lane, nxt);
 
         // ---- 1. forward into the stage; ties resolved in place
         int32_t var_num;
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         retire_stores();
         wave_sync();
         store_stage(stage, wv, lane, recon, (nb < 32u ? nb : 32u) * 256u);
-        if (!DCTQ_RT_EARLY_PREFETCH) prefetch_batch(ps, g + step, lane, nxt);
+        if (!DCTQ_RT_EARLY_PREFETCH) prefetch_batch<false>(ps, g + step, lane, nxt);
         // keep inverse B's inputs packed until here (converted early they are 64 more live VGPRs)
 #pragma unroll
         for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(qb[r].x), "+v"(qb[r].y), "+v"(qb[r].z), "+v"(qb[r].w));
