@@ -40,7 +40,9 @@ extern "C" {
  * or streams synchronised by the caller); use one plan per concurrent stream. */
 typedef struct dctq_plan dctq_plan;
 
-/* quality is clamped to 1..100 exactly as quant_init does (src/quantization.c:26-31). */
+/* quality is clamped to 1..100 exactly as quant_init does (src/quantization.c:26-31).
+ * A plan holds its tables and the forward kernel's tie stash in device memory
+ * (about 256 MiB on a 256-CU MI355X); a plan is reusable and cheap to keep. */
 int dctq_plan_create(int quality, int adaptive, dctq_plan **plan);
 /* Bind an existing reference-style context (block_size must be 8); its
  * quant_matrix VALUES are used, so a caller-modified table is honoured. */
