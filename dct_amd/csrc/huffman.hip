@@ -43,6 +43,9 @@
 #ifndef DCTQ_HUF_ABLATE
 #define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge
 #endif
+#ifndef DCTQ_HUF_DMA_POLICY
+#define DCTQ_HUF_DMA_POLICY "nt"  // cache policy of the tile DMA (read once)
+#endif
 
 namespace dctq {
 
@@ -181,7 +184,7 @@ __device__ __forceinline__ void tile_dma(const int16_t *coef, long long t, long 
         asm volatile(
             "s_mov_b32 %0, m0\n\t"
             "s_mov_b32 m0, %1\n\t"
-            "buffer_load_dwordx4 %2, %3, 0 offen nt lds\n\t"
+            "buffer_load_dwordx4 %2, %3, 0 offen " DCTQ_HUF_DMA_POLICY " lds\n\t"
             "s_mov_b32 m0, %0"
             : "=&s"(save)
             : "s"(lds + c * 1024), "v"(c * 1024 + (base ^ ((c & 1) << 6))), "s"(rs)
