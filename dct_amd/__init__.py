@@ -56,6 +56,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
         "dctq_rle_emit": ([vp, ll, vp, vp, vp], i),
         "dctq_rle_decode": ([vp, vp, ll, vp, vp], i),
         "dctq_huffman_bits": ([vp, ll, vp, vp], i),
+        "dctq_huffman_bits_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
     }
     if diagnostic:
         sig.update({
@@ -238,6 +239,20 @@ class Plan:
                                         _stream_ptr(stream)))
         total = int(off[nb].item()) & 0xFFFFFFFF
         return outs, off, sym[:min(total, cap)]
+
+    def huffman_bits_planes(self, planes, out=None, stream=None):
+        """Per-block Huffman size straight from up to 4 u8 planes (the whole per-block loop of
+        tests/test_entropy.c:300-341 on the GPU, coefficients kept on chip): int32 [N], blocks
+        numbered plane by plane, equal to huffman_bits(cat(forward_quant_planes(planes)))."""
+        import torch
+        n = len(planes)
+        descs = (_Plane * n)(*[plane_desc(px) for px in planes])
+        nb = sum(d.nframes * (d.width // 8) * (d.height // 8) for d in descs)
+        if out is None:
+            out = torch.empty(nb, dtype=torch.int32, device=planes[0].device)
+        self._chk(self._L.dctq_huffman_bits_planes(self._h, descs, n, C.c_void_p(out.data_ptr()),
+                                                   _stream_ptr(stream)))
+        return out
 
     def forward_float(self, px, out=None, stream=None):
         import torch

@@ -431,6 +431,28 @@ int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, vo
     return DCTQ_OK;
 }
 
+int dctq_huffman_bits_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *bits,
+                             void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = dctq::check_plan(plan)) return rc;
+    if (!bits || ((uintptr_t)bits) % 4) return fail(DCTQ_EINVAL, "bits is NULL or not 4-byte aligned");
+    // plane_set's coefficient pointers are not used by this launch (they stay on chip)
+    int16_t *const none[dctq::kMaxPlanes] = {(int16_t *)16, (int16_t *)16, (int16_t *)16, (int16_t *)16};
+    dctq::EncodeSet es = {};
+    int rc = dctq::plane_set(planes, nplanes, none, nullptr, &es.ps);
+    if (rc) return rc;
+    long long blocks = 0;
+    for (int k = 0; k < nplanes; ++k) {
+        es.blk_first[k] = (uint32_t)blocks;
+        blocks += es.ps.pl[k].nblk;
+        if (blocks >= (1ll << 31)) return fail(DCTQ_EINVAL, "2^31 blocks or more in one launch");
+    }
+    es.blk_first[nplanes] = (uint32_t)blocks;
+    HIPCHK(dctq::launch_huffman_from_pixels(es, plan->dev, plan->adaptive, bits, (hipStream_t)stream, plan->num_cus),
+           "huffman_from_pixels launch");
+    return DCTQ_OK;
+}
+
 int dctq_device_count(int *count) {
     DCTQ_ENTRY;
     HIPCHK(hipGetDeviceCount(count), "hipGetDeviceCount");

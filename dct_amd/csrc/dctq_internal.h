@@ -146,6 +146,8 @@ hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *
                            unsigned long long capacity, hipStream_t stream, int num_cus);
 // per-block Huffman size estimate (huffman.hip)
 hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bits, hipStream_t stream, int num_cus);
+hipError_t launch_huffman_from_pixels(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *bits,
+                                      hipStream_t stream, int num_cus);
 hipError_t launch_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblk, int16_t *coef,
                              hipStream_t stream, int num_cus);
 hipError_t launch_fdct8_float(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);

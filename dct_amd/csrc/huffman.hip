@@ -39,6 +39,7 @@
 // (DESIGN.md 3.8).
 // DCTQ_HUF_MIN_WAVES (launch bound, default 3 waves/SIMD: 168 VGPRs) is an A/B knob.
 #include "dctq_internal.h"
+#include "fdct8_core.h"
 
 #ifndef DCTQ_HUF_ABLATE
 #define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge
@@ -412,6 +413,167 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
 // passes on one box (profiles/r02/huffman_dma_ab.log).
 #define DCTQ_HUF_BITS_AUX 2
 #endif
+// One tile in the wave's stage (Huffman layout, blocks past the end zeroed): the
+// bit count of every lane's block.  next_tile() is called once the stage may be
+// overwritten (the next tile's DMA, or nothing).
+template <typename NextTile>
+__device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, int wv, int nb, NextTile next_tile) {
+    bool dma_issued = false;
+    uint32_t nz = 0;
+    bool last_zero;     // c[63] == 0: value 0 is a symbol once
+    bool narrow = false;  // a dense tile whose every block has its values (zeros included) within 64 integers
+    int32_t vmin = 0;
+    uint32_t span = 64;  // the lane's values (zeros included) lie in [vmin, vmin + span)
+    {
+        uint32_t d[32];
+        tile_row(mine, lane, d);
+        {
+            // nonzeros: unsigned min(h, 1) is 1 for any nonzero half; two packed 16-bit partial sums
+            typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+            const u2 one = {1, 1};
+            u2 acc = {0, 0};
+            const uint32_t one32 = __builtin_bit_cast(uint32_t, one);
+#pragma unroll
+            for (int k = 0; k < 32; ++k) {
+                uint32_t m;  // inline asm: LLVM turns the packed min into compares and selects
+                asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d[k]), "v"(one32));
+                acc += __builtin_bit_cast(u2, m);
+            }
+            nz = (uint32_t)acc.x + (uint32_t)acc.y;
+        }
+        last_zero = (d[31] >> 16) == 0u;
+        if (__builtin_amdgcn_ballot_w64(nz > 32)) {
+            // dense tile: the span of its values, zeros included (packed 16-bit min/max)
+            typedef short s2 __attribute__((ext_vector_type(2)));
+            s2 mn = __builtin_bit_cast(s2, d[0]), mx = mn;
+#pragma unroll
+            for (int k = 1; k < 32; ++k) {
+                const s2 x = __builtin_bit_cast(s2, d[k]);
+                mn = __builtin_elementwise_min(mn, x);
+                mx = __builtin_elementwise_max(mx, x);
+            }
+            vmin = mn.x < mn.y ? mn.x : mn.y;
+            const int32_t vmax = mx.x > mx.y ? mx.x : mx.y;
+            span = (uint32_t)(vmax - vmin + 1);
+            narrow = !__builtin_amdgcn_ballot_w64(lane < nb && vmax - vmin >= 64);
+        }
+    }
+    // the paths re-read the row: a memory clobber keeps the compiler from reusing
+    // (and holding) these 32 registers across the choice
+    asm volatile("" ::: "memory");
+    // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
+    uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
+    uint32_t nodes = last_zero ? 1u : 0u;
+    uint32_t lmax = last_zero ? 1u : 0u;  // the largest leaf weight (dense paths)
+    const bool dense = __builtin_amdgcn_ballot_w64(nz > 32) != 0;
+#ifdef DCTQ_HUF_UNIFORM_MERGE
+    const bool lane_merge = false;
+#else
+    const bool lane_merge = dense;  // the dense paths merge per lane (occupancy mask)
+#endif
+    uint32_t wpl = 0, pending = 0;
+#ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
+    if (true) {
+    } else
+#endif
+    if (narrow) {
+        dma_issued = true;
+        narrow_tile(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl, next_tile);  // the zero leaf included
+    } else {
+        if (!__builtin_amdgcn_ballot_w64(nz > 16))
+            sparse_runs<16>(mine, lane, nodes, lmax);
+        else if (!__builtin_amdgcn_ballot_w64(nz > 32))
+            sparse_runs<32>(mine, lane, nodes, lmax);
+        else
+            dense_runs(mine, lane, nodes, lmax);
+        if (last_zero) hist_add(mine, 1, lane, 1);
+    // ---- bucket merge (see the header): wpl = sum of internal node weights.
+    if (lane >= nb) nodes = 1;  // past the tail: nothing to do
+    const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [w*64]
+    if (lane_merge) {
+        // occupancy of the leaf buckets, read back up to the wave's largest leaf weight
+        // (cheaper than marking every leaf; this wave's LDS atomics are already ordered)
+        uint64_t occ = 0;
+#pragma unroll
+        for (uint32_t w = 1; w <= 8; ++w)  // independent reads, in flight together
+            occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
+        for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w)
+            occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
+        if (lane >= nb) occ = 0;  // past the tail (the narrow path keeps them: it must clear its rows)
+        // Each lane jumps to its own next occupied bucket (lowest bit of occ), so the
+        // loop runs as many steps as the busiest lane has occupied buckets, not up to
+        // its largest weight.  New weights (pending + w, 2w) are above w, so the scan
+        // order is the bucket order; weights never exceed the symbol count (<= 64).
+        // The lane is done when no bucket is left: its last node (the root) is then
+        // `pending`.  The step cap only bounds the loop.
+        for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ != 0); ++step) {
+            if (occ) {
+                const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
+                occ &= occ - 1ull;  // bucket w is emptied by this step
+                uint32_t c = bucket[w * 64];
+                if (pending && c) {
+                    const uint32_t nw = pending + w;
+                    wpl += nw;
+                    hist_add(mine, nw, lane, 1);
+                    mark(occ, nw, 1);
+                    --c;
+                    pending = 0;
+                }
+                const uint32_t pairs = c >> 1;
+                if (pairs) {
+                    wpl += pairs * 2 * w;
+                    hist_add(mine, 2 * w, lane, pairs);
+                    mark(occ, 2 * w, 1);
+                }
+                if (c & 1) pending = w;
+            }
+        }
+    } else {
+    // Sparse tiles (few weights): every weight in turn; bucket w+1 is read at the top of iteration w, so its
+    // LDS latency hides behind the iteration; the only merges of iteration w that
+    // land on w+1 (pending 1 + w, and the pairs of w = 1) are carried in a register
+    uint32_t cur = bucket[64];
+    for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
+        const uint32_t nxt = w < 64 ? bucket[(w + 1) * 64] : 0u;
+        uint32_t c = cur, carry = 0;
+        if (nodes > 1) {
+            if (pending && c) {
+                const uint32_t nw = pending + w;
+                wpl += nw;
+                if (nw == w + 1)
+                    carry = 1;
+                else
+                    hist_add(mine, nw, lane, 1);
+                --c;
+                --nodes;
+                pending = 0;
+            }
+            const uint32_t pairs = c >> 1;
+            if (pairs) {
+                wpl += pairs * 2 * w;
+                nodes -= pairs;
+                if (w == 1)
+                    carry += pairs;
+                else
+                    hist_add(mine, 2 * w, lane, pairs);
+            }
+            if (c & 1) pending = w;
+        }
+        cur = nxt + carry;
+    }
+    }
+    }
+    if (!dma_issued) {  // the histogram paths used the stage until now
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): their bucket reads are done
+        __builtin_amdgcn_wave_barrier();
+        next_tile();
+    }
+    return 8u * count + wpl;
+}
+
+#ifndef DCTQ_HP_PREFETCH
+#define DCTQ_HP_PREFETCH 0  // A/B: huffman_from_pixels prefetches the next batch's rows into registers
+#endif
 #ifndef DCTQ_HUF_MIN_WAVES
 #define DCTQ_HUF_MIN_WAVES 3
 #endif
@@ -444,161 +606,12 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_wave_barrier();
         }
-        bool dma_issued = false;
-        uint32_t nz = 0;
-        bool last_zero;     // c[63] == 0: value 0 is a symbol once
-        bool narrow = false;  // a dense tile whose every block has its values (zeros included) within 64 integers
-        int32_t vmin = 0;
-        uint32_t span = 64;  // the lane's values (zeros included) lie in [vmin, vmin + span)
-        {
-            uint32_t d[32];
-            tile_row(mine, lane, d);
-            {
-                // nonzeros: unsigned min(h, 1) is 1 for any nonzero half; two packed 16-bit partial sums
-                typedef unsigned short u2 __attribute__((ext_vector_type(2)));
-                const u2 one = {1, 1};
-                u2 acc = {0, 0};
-                const uint32_t one32 = __builtin_bit_cast(uint32_t, one);
-#pragma unroll
-                for (int k = 0; k < 32; ++k) {
-                    uint32_t m;  // inline asm: LLVM turns the packed min into compares and selects
-                    asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d[k]), "v"(one32));
-                    acc += __builtin_bit_cast(u2, m);
-                }
-                nz = (uint32_t)acc.x + (uint32_t)acc.y;
-            }
-            last_zero = (d[31] >> 16) == 0u;
-            if (__builtin_amdgcn_ballot_w64(nz > 32)) {
-                // dense tile: the span of its values, zeros included (packed 16-bit min/max)
-                typedef short s2 __attribute__((ext_vector_type(2)));
-                s2 mn = __builtin_bit_cast(s2, d[0]), mx = mn;
-#pragma unroll
-                for (int k = 1; k < 32; ++k) {
-                    const s2 x = __builtin_bit_cast(s2, d[k]);
-                    mn = __builtin_elementwise_min(mn, x);
-                    mx = __builtin_elementwise_max(mx, x);
-                }
-                vmin = mn.x < mn.y ? mn.x : mn.y;
-                const int32_t vmax = mx.x > mx.y ? mx.x : mx.y;
-                span = (uint32_t)(vmax - vmin + 1);
-                narrow = !__builtin_amdgcn_ballot_w64(lane < nb && vmax - vmin >= 64);
-            }
-        }
-        // the paths re-read the row: a memory clobber keeps the compiler from reusing
-        // (and holding) these 32 registers across the choice
-        asm volatile("" ::: "memory");
-        // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
-        uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
-        uint32_t nodes = last_zero ? 1u : 0u;
-        uint32_t lmax = last_zero ? 1u : 0u;  // the largest leaf weight (dense paths)
-        const bool dense = __builtin_amdgcn_ballot_w64(nz > 32) != 0;
-#ifdef DCTQ_HUF_UNIFORM_MERGE
-        const bool lane_merge = false;
-#else
-        const bool lane_merge = dense;  // the dense paths merge per lane (occupancy mask)
-#endif
-        uint32_t wpl = 0, pending = 0;
-#ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
-        if (true) {
-        } else
-#endif
-        if (narrow) {
-            dma_issued = true;
-            narrow_tile(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl, [&] {
-                if (t + stride < ntiles) tile_dma(coef, t + stride, nblk, mine, lane);
-            });  // the zero leaf included
-        } else {
-            if (!__builtin_amdgcn_ballot_w64(nz > 16))
-                sparse_runs<16>(mine, lane, nodes, lmax);
-            else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-                sparse_runs<32>(mine, lane, nodes, lmax);
-            else
-                dense_runs(mine, lane, nodes, lmax);
-            if (last_zero) hist_add(mine, 1, lane, 1);
-        // ---- bucket merge (see the header): wpl = sum of internal node weights.
-        if (lane >= nb) nodes = 1;  // past the tail: nothing to do
-        const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [w*64]
-        if (lane_merge) {
-            // occupancy of the leaf buckets, read back up to the wave's largest leaf weight
-            // (cheaper than marking every leaf; this wave's LDS atomics are already ordered)
-            uint64_t occ = 0;
-#pragma unroll
-            for (uint32_t w = 1; w <= 8; ++w)  // independent reads, in flight together
-                occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
-            for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w)
-                occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
-            if (lane >= nb) occ = 0;  // past the tail (the narrow path keeps them: it must clear its rows)
-            // Each lane jumps to its own next occupied bucket (lowest bit of occ), so the
-            // loop runs as many steps as the busiest lane has occupied buckets, not up to
-            // its largest weight.  New weights (pending + w, 2w) are above w, so the scan
-            // order is the bucket order; weights never exceed the symbol count (<= 64).
-            // The lane is done when no bucket is left: its last node (the root) is then
-            // `pending`.  The step cap only bounds the loop.
-            for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ != 0); ++step) {
-                if (occ) {
-                    const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
-                    occ &= occ - 1ull;  // bucket w is emptied by this step
-                    uint32_t c = bucket[w * 64];
-                    if (pending && c) {
-                        const uint32_t nw = pending + w;
-                        wpl += nw;
-                        hist_add(mine, nw, lane, 1);
-                        mark(occ, nw, 1);
-                        --c;
-                        pending = 0;
-                    }
-                    const uint32_t pairs = c >> 1;
-                    if (pairs) {
-                        wpl += pairs * 2 * w;
-                        hist_add(mine, 2 * w, lane, pairs);
-                        mark(occ, 2 * w, 1);
-                    }
-                    if (c & 1) pending = w;
-                }
-            }
-        } else {
-        // Sparse tiles (few weights): every weight in turn; bucket w+1 is read at the top of iteration w, so its
-        // LDS latency hides behind the iteration; the only merges of iteration w that
-        // land on w+1 (pending 1 + w, and the pairs of w = 1) are carried in a register
-        uint32_t cur = bucket[64];
-        for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
-            const uint32_t nxt = w < 64 ? bucket[(w + 1) * 64] : 0u;
-            uint32_t c = cur, carry = 0;
-            if (nodes > 1) {
-                if (pending && c) {
-                    const uint32_t nw = pending + w;
-                    wpl += nw;
-                    if (nw == w + 1)
-                        carry = 1;
-                    else
-                        hist_add(mine, nw, lane, 1);
-                    --c;
-                    --nodes;
-                    pending = 0;
-                }
-                const uint32_t pairs = c >> 1;
-                if (pairs) {
-                    wpl += pairs * 2 * w;
-                    nodes -= pairs;
-                    if (w == 1)
-                        carry += pairs;
-                    else
-                        hist_add(mine, 2 * w, lane, pairs);
-                }
-                if (c & 1) pending = w;
-            }
-            cur = nxt + carry;
-        }
-        }
-        }
-        if (!dma_issued) {  // the histogram paths used the stage until now
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): their bucket reads are done
-            __builtin_amdgcn_wave_barrier();
+        const uint32_t out = tile_bits(mine, ctr, lane, wv, nb, [&] {
             if (t + stride < ntiles) tile_dma(coef, t + stride, nblk, mine, lane);
-        }
+        });
         const __amdgpu_buffer_rsrc_t rb =
             __builtin_amdgcn_make_buffer_rsrc(bits + t * 64, (short)0, nb * 4, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(8u * count + wpl, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
+        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
     }
 }
 
@@ -617,4 +630,107 @@ hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bi
                        nblk, bits, ntiles);
     return hipGetLastError();
 }
+
+// ============================================================================
+// The reference pipeline's per-block size straight from pixels (SURVEY 8(f)4 fed
+// by 8(a)): forward DCT + quantization (fdct8_core.h, ties resolved in place in
+// the reference's order) -> the tile in this kernel's layout -> tile_bits.  The
+// coefficients never leave LDS: 64 B read and 4 B written per block, against
+// 192 + 132 for dctq_forward_quant_planes followed by dctq_huffman_bits.
+// Same grid, occupancy (3 waves/SIMD) and LDS as huffman_bits_kernel, plus the
+// exact path's 1 KiB table copy.
+template <bool ADAPTIVE>
+__global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_pixels_kernel(EncodeSet es,
+                                                                                              const DevTables *__restrict__ dev,
+                                                                                              uint32_t *__restrict__ bits) {
+    __shared__ uint4 lds[kHufWaves * kHufWaveLds / 16];
+    __shared__ uint4 ctr_lds[kHufCtrBytes / 16];
+    __shared__ ExactTables tab;
+    static_assert(64 * kPitch2 + 128 <= kHufWaveLds, "forward stage + tie scratch fit the wave's region");
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    char *mine = reinterpret_cast<char *>(lds) + wv * kHufWaveLds;
+    char *ctr = reinterpret_cast<char *>(ctr_lds);
+    // the forward core addresses the stage as (wv * 64 + lane) * kPitch2 from its base
+    uint4 *stage = reinterpret_cast<uint4 *>(mine - wv * 64 * kPitch2);
+    uint16_t *scr = reinterpret_cast<uint16_t *>(mine + 64 * kPitch2);
+    for (int i = threadIdx.x; i < kHufCtrBytes / 16; i += kHufThreads) ctr_lds[i] = make_uint4(0, 0, 0, 0);
+    load_exact_tables(&tab, dev);  // ends with __syncthreads
+    const PlaneSet &ps = es.ps;
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t step = gridDim.x * kHufWaves;
+#if DCTQ_HP_PREFETCH
+    uint2 nxt[8];
+    prefetch_batch(ps, blockIdx.x * kHufWaves + wv, lane, nxt);
+#endif
+    for (uint32_t g = blockIdx.x * kHufWaves + wv; g < nbatch; g += step) {
+        const int k = plane_of(ps, g);
+        const PlaneArgs &p = ps.pl[k];
+        const uint32_t b = g - ps.first[k];
+        const uint32_t n = b * 64 + lane;
+        const bool valid = n < (uint32_t)p.nblk;
+        const int nb = (uint32_t)p.nblk - b * 64 < 64u ? (int)((uint32_t)p.nblk - b * 64) : 64;
+        uint2 cur[8];
+#if DCTQ_HP_PREFETCH
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+#else
+        load_rows(p, n, cur);
+#endif
+        // the rows are in, and the previous batch's bits store has left before
+        // LDS reads land in VGPRs (the store-data hazard)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        uint32_t mlo, mhi;
+        int32_t var_num;
+        fdct8_compute<ADAPTIVE, false>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
+        flat_dc_fix(dev, cur, stage, lane, wv, mlo);
+        if (!valid) mlo = mhi = 0;
+        if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) (void)resolve_ties_compact<ADAPTIVE>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
+        wave_sync();
+        // the block's 128 B from the forward stage (pitch kPitch2, 8-B aligned) to
+        // this kernel's layout: piece q of block b at b * 128 + 16 * (q ^ ((b >> 1) & 7))
+        uint4 row[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint2 lo = *reinterpret_cast<const uint2 *>(mine + lane * kPitch2 + 16 * q);
+            const uint2 hi = *reinterpret_cast<const uint2 *>(mine + lane * kPitch2 + 16 * q + 8);
+            row[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane's reads are done before any write
+        wave_sync();
+        const int sw = (lane >> 1) & 7;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            *reinterpret_cast<uint4 *>(mine + lane * 128 + 16 * (q ^ sw)) =
+                lane < nb ? row[q] : make_uint4(0, 0, 0, 0);  // blocks past the end are empty
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        wave_sync();
+#if DCTQ_HP_PREFETCH
+        prefetch_batch(ps, g + step, lane, nxt);  // in flight through the size computation
+#endif
+        const uint32_t out = tile_bits(mine, ctr, lane, wv, nb, [] {});
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+            bits + es.blk_first[k] + (size_t)b * 64, (short)0, nb * 4, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
+        // tile_bits leaves the stage to the next batch's forward only after its own reads
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        wave_sync();
+    }
+}
+
+hipError_t launch_huffman_from_pixels(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *bits,
+                                      hipStream_t stream, int num_cus) {
+    const uint32_t nbatch = es.ps.first[es.ps.n];
+    long long grid = ((long long)nbatch + kHufWaves - 1) / kHufWaves;
+    const long long cap = (long long)num_cus * DCTQ_HUF_GRID_PER_CU;
+    if (grid > cap) grid = cap;
+    if (grid < 1) return hipSuccess;
+    if (adaptive)
+        hipLaunchKernelGGL(huffman_from_pixels_kernel<true>, dim3((unsigned)grid), dim3(kHufThreads), 0, stream, es, dev,
+                           bits);
+    else
+        hipLaunchKernelGGL(huffman_from_pixels_kernel<false>, dim3((unsigned)grid), dim3(kHufThreads), 0, stream, es,
+                           dev, bits);
+    return hipGetLastError();
+}
+
 }  // namespace dctq

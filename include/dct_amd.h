@@ -144,6 +144,15 @@ int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long 
  * on the reference heap's tie order, their sum does not (Huffman trees are
  * optimal); the codes themselves are not produced.  coef 16-byte aligned. */
 int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, void *stream);
+/* The same per-block size straight from pixels: the whole per-block loop of
+ * tests/test_entropy.c:300-341 (create_block_from_pixels -> dct_forward ->
+ * quantize -> run_length_encode -> build_huffman_codes -> get_encoded_size) for
+ * every block of up to 4 planes, blocks numbered plane 0 first (as
+ * dctq_encode_planes).  Equal to dctq_forward_quant_planes followed by
+ * dctq_huffman_bits over the concatenated coefficients, but the coefficients
+ * never leave the chip.  bits: 4-byte aligned, one entry per block. */
+int dctq_huffman_bits_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *bits,
+                             void *stream);
 
 /* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented
  * by the number of coefficients resolved by the exact fp64 tie path in later

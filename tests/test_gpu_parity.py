@@ -961,6 +961,39 @@ def test_huffman_bits_tile_sequences(T, dm):
     assert np.array_equal(got, want_base[order].reshape(-1)[:nblk])
 
 
+def test_huffman_bits_planes_from_pixels(T, dm):
+    """dctq_huffman_bits_planes (forward + quantization + per-block Huffman size in ONE launch,
+    coefficients on chip) == dctq_huffman_bits over dctq_forward_quant_planes' output, bit-exact,
+    blocks numbered plane by plane: every input kind, tie-heavy plans (extreme q10/q100, in-place
+    exact resolution), adaptive plans, up to 4 planes of ragged geometry (partial last batches and
+    tiles), and a stack large enough for many batches per wave.  One small plane also against the
+    oracle's literal pipeline (forward_plane -> huffman_bits_plane)."""
+    import oracle as O
+    rng = np.random.default_rng(5)
+    for kind, q, ad in [("uniform", 50, 0), ("extreme", 10, 0), ("smooth", 90, 1), ("const", 50, 0),
+                        ("uniform", 100, 0), ("extreme", 100, 1), ("uniform", 1, 0), ("smooth", 75, 1)]:
+        plan = dm.Plan(q, ad)
+        planes = [dm.synth(int(rng.integers(1 << 30)), kind, 8 * 61, 8 * 9, 3),
+                  dm.synth(int(rng.integers(1 << 30)), kind, 8 * 13, 8 * 5, 2),
+                  dm.synth(int(rng.integers(1 << 30)), kind, 8 * 40, 8 * 8)]
+        want = dm.huffman_bits(T.cat(plan.forward_quant_planes(planes)))
+        got = plan.huffman_bits_planes(planes)
+        T.cuda.synchronize()
+        assert T.equal(got, want), (kind, q, ad)
+    # against the oracle: one plane, the reference's pipeline restated
+    px = O.synth_plane(11, O.KINDS["uniform"], 8 * 37, 8 * 11)
+    want = O.huffman_bits_plane(O.forward_plane(px, 50, 0))
+    got = dm.Plan(50, 0).huffman_bits_planes([gpu_px(T, px)]).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want)
+    # a 4K 4:2:0 stack (many batches per wave on the 16-per-CU grid)
+    plan = dm.Plan(50, 0)
+    planes = [dm.synth(3, "uniform", 3840, 2160, 4), dm.synth(4, "uniform", 1920, 1080, 8)]
+    want = dm.huffman_bits(T.cat(plan.forward_quant_planes(planes)))
+    got = plan.huffman_bits_planes(planes)
+    T.cuda.synchronize()
+    assert T.equal(got, want)
+
+
 def test_encode_planes_fused(T, dm):
     """dctq_encode_planes (forward + zigzag/RLE, the count fused into the forward) equals the
     oracle's run_length_encode of the oracle's quantized planes, blocks numbered plane
