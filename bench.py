@@ -423,6 +423,20 @@ def encode_leg(args, plan, luma, chroma, world, dev):
                       "blocks_per_s": world * n * args.encode_steps / el_h,
                       "ms_per_step": el_h / args.encode_steps * 1e3, "bits_per_block": mean_bits,
                       "compression_vs_u8": 512.0 / mean_bits, "_check": huf_check}
+    # the same sizes straight from the pixels in one launch (coefficients on chip)
+    fused_bits = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def huffman_from_pixels():
+        rc = L.dctq_huffman_bits_planes(plan._h, descs, 2, C.c_void_p(fused_bits.data_ptr()), stream)
+        if rc:
+            raise RuntimeError(f"dctq_huffman_bits_planes rc={rc}")
+
+    el_f = timed(huffman_from_pixels)
+    out["huffman_from_pixels"] = {
+        "op": "huffman_bits_planes (forward + quantization + per-block Huffman size in one launch) over all planes",
+        "blocks_per_s": world * n * args.encode_steps / el_f, "ms_per_step": el_f / args.encode_steps * 1e3,
+        "hbm_bytes_per_block": 68,
+        "equals_forward_then_huffman_bits": bool(torch.equal(fused_bits, torch.cat(bits)))}
     if dist.is_initialized():
         def encode_gather():
             encode()
