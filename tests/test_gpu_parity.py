@@ -554,7 +554,7 @@ def test_invalid_arguments(T, dm):
         dm.Plan(50, 1).inverse(torch.zeros((4, 64), dtype=torch.int16, device="cuda"))
     # the multi-plane calls: 0 or 5 planes, a bad plane among good ones, NULL outputs
     g = torch.zeros((16, 16), dtype=torch.uint8, device="cuda")
-    for fn in (plan.round_trip_planes, plan.encode_planes):
+    for fn in (plan.round_trip_planes, plan.encode_planes, plan.huffman_bits_planes):
         with pytest.raises(dm.DctqError):
             fn([g] * 5)
         with pytest.raises(dm.DctqError):
@@ -568,6 +568,9 @@ def test_invalid_arguments(T, dm):
     assert L.dctq_encode_planes(plan._h, d, 1, cp, C.c_void_p(off.data_ptr()), None, 0, None, None) != 0  # no ws
     assert L.dctq_encode_planes(plan._h, d, 1, cp, C.c_void_p(off.data_ptr()), None, -1, C.c_void_p(off.data_ptr()),
                                 None) != 0                                                 # negative capacity
+    assert L.dctq_huffman_bits_planes(plan._h, d, 1, None, None) != 0                     # bits NULL
+    assert L.dctq_huffman_bits_planes(plan._h, d, 1, C.c_void_p(off.data_ptr() + 2), None) != 0  # misaligned
+    assert L.dctq_huffman_bits_planes(None, d, 1, C.c_void_p(off.data_ptr()), None) != 0  # no plan
 
 
 # ------------------------------------------------------------ legacy per-block API
