@@ -143,7 +143,19 @@ __device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine,
 // conflict-free), come back as N registers padded with kSent and take the
 // N-network instead of the 64-one.
 // The lane's 64 coefficients from its row of the tile stage, as 32 dwords.
+// FWD: the row sits where the forward core left it (huffman_from_pixels_kernel):
+// lane * kPitch2, 8-byte aligned, unswizzled.
+template <bool FWD = false>
 __device__ __forceinline__ void tile_row(const char *mine, int lane, uint32_t (&d)[32]) {
+    if constexpr (FWD) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint2 w = *reinterpret_cast<const uint2 *>(mine + lane * kPitch2 + 8 * k);
+            d[2 * k] = w.x;
+            d[2 * k + 1] = w.y;
+        }
+        return;
+    }
     // the row's address, made opaque per call: eight hoisted loop-invariant piece
     // addresses spilled; recomputed it is one v_xor per piece
     int row = (lane << 7) | (((lane >> 1) & 7) << 4);
@@ -196,10 +208,10 @@ __device__ __forceinline__ void tile_dma(const int16_t *coef, long long t, long 
 // Each path re-reads the tile row itself, so nothing but scalars is live across
 // the path choice and each path gets its own register allocation (a shared
 // 32-register row made the compiler hold 188-336 VGPRs).
-template <int N>
+template <int N, bool FWD = false>
 __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &nodes, uint32_t &lmax) {
     uint32_t d[32];
-    tile_row(mine, lane, d);
+    tile_row<FWD>(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
     __builtin_amdgcn_wave_barrier();
     // branch-free compaction: every key is written at the next slot, which advances
@@ -226,11 +238,12 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
     runs_to_hist<N, false>(b, mine, lane, nodes, lmax);
 }
 
+template <bool FWD = false>
 __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes, uint32_t &lmax) {
     uint32_t a[64];
     {
         uint32_t d[32];
-        tile_row(mine, lane, d);
+        tile_row<FWD>(mine, lane, d);
 #pragma unroll
         for (int h = 0; h < 32; ++h) {
             a[2 * h] = (d[h] << 16) - 1u;
@@ -258,11 +271,11 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
 //  4. merge as in the dense path (each lane jumps to its next occupied bucket),
 //     every bucket read AND cleared as it is processed.
 // Returns the symbol count and the WPL.
-template <typename NextTile>
+template <bool FWD = false, typename NextTile>
 __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lane, int wv, int32_t vmin, uint32_t span,
                                             bool last_zero, uint32_t &count, uint32_t &wpl, NextTile next_tile) {
     uint32_t d[32];
-    tile_row(mine, lane, d);
+    tile_row<FWD>(mine, lane, d);
     // the row is in registers and the stage is free: the next tile streams in meanwhile
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     next_tile();
@@ -416,7 +429,7 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
 // One tile in the wave's stage (Huffman layout, blocks past the end zeroed): the
 // bit count of every lane's block.  next_tile() is called once the stage may be
 // overwritten (the next tile's DMA, or nothing).
-template <typename NextTile>
+template <bool FWD = false, typename NextTile>
 __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, int wv, int nb, NextTile next_tile) {
     bool dma_issued = false;
     uint32_t nz = 0;
@@ -426,7 +439,7 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
     uint32_t span = 64;  // the lane's values (zeros included) lie in [vmin, vmin + span)
     {
         uint32_t d[32];
-        tile_row(mine, lane, d);
+        tile_row<FWD>(mine, lane, d);
         {
             // nonzeros: unsigned min(h, 1) is 1 for any nonzero half; two packed 16-bit partial sums
             typedef unsigned short u2 __attribute__((ext_vector_type(2)));
@@ -478,14 +491,14 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
 #endif
     if (narrow) {
         dma_issued = true;
-        narrow_tile(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl, next_tile);  // the zero leaf included
+        narrow_tile<FWD>(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl, next_tile);  // the zero leaf included
     } else {
         if (!__builtin_amdgcn_ballot_w64(nz > 16))
-            sparse_runs<16>(mine, lane, nodes, lmax);
+            sparse_runs<16, FWD>(mine, lane, nodes, lmax);
         else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-            sparse_runs<32>(mine, lane, nodes, lmax);
+            sparse_runs<32, FWD>(mine, lane, nodes, lmax);
         else
-            dense_runs(mine, lane, nodes, lmax);
+            dense_runs<FWD>(mine, lane, nodes, lmax);
         if (last_zero) hist_add(mine, 1, lane, 1);
     // ---- bucket merge (see the header): wpl = sum of internal node weights.
     if (lane >= nb) nodes = 1;  // past the tail: nothing to do
@@ -571,6 +584,9 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
     return 8u * count + wpl;
 }
 
+#ifndef DCTQ_HP_DIRECT
+#define DCTQ_HP_DIRECT 1  // the size path reads the rows where the forward left them; 0: copy them to the tile layout first (A/B: direct is -2.8 to -4.5 %)
+#endif
 #ifndef DCTQ_HP_PREFETCH
 #define DCTQ_HP_PREFETCH 0  // A/B: huffman_from_pixels prefetches the next batch's rows into registers
 #endif
@@ -686,6 +702,17 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         if (!valid) mlo = mhi = 0;
         if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) (void)resolve_ties_compact<ADAPTIVE>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
         wave_sync();
+#if DCTQ_HP_DIRECT
+        if (nb < 64) {  // blocks past the end are empty
+            if (lane >= nb) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) *reinterpret_cast<uint2 *>(mine + lane * kPitch2 + 8 * q) = make_uint2(0, 0);
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            wave_sync();
+        }
+        const uint32_t out = tile_bits<true>(mine, ctr, lane, wv, nb, [] {});
+#else
         // the block's 128 B from the forward stage (pitch kPitch2, 8-B aligned) to
         // this kernel's layout: piece q of block b at b * 128 + 16 * (q ^ ((b >> 1) & 7))
         uint4 row[8];
@@ -708,6 +735,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         prefetch_batch(ps, g + step, lane, nxt);  // in flight through the size computation
 #endif
         const uint32_t out = tile_bits(mine, ctr, lane, wv, nb, [] {});
+#endif
         const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
             bits + es.blk_first[k] + (size_t)b * 64, (short)0, nb * 4, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
