@@ -91,7 +91,63 @@ def parse():
                          "(gather, band, symbol-stream gather): the RCCL code path on a single GPU")
     ap.add_argument("--backend", default="nccl", help="N>1 process group (nccl = RCCL; gloo only to rehearse "
                                                       "several ranks on one GPU)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rank plumbing only, no GPU: every rank joins a gloo group and rank 0 prints the world it "
+                         "formed (tests/test_bench_launch.py)")
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) with no launcher around this process: start N copies of
+    this command as child processes, one per GPU, with the environment
+    torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, a free MASTER_PORT), wait for all of
+    them, and return the exit status.  This parent never touches the GPU (no HIP
+    call, not even a device count) and never exec()s: the children are ordinary
+    subprocesses.  Rank 0 inherits stdout, so its one JSON line is this command's
+    output; if any rank fails, the others are stopped (by PID) and the status is
+    the failing rank's."""
+    import signal
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
+def launch_check(args) -> None:
+    """--launch-check: each rank joins a gloo group over the env rendezvous and
+    contributes its rank; rank 0 prints the world it saw.  No GPU."""
+    dist.init_process_group("gloo")
+    t = torch.tensor([dist.get_rank()], dtype=torch.int64)
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"n_gpus": args.gpus, "world_size": dist.get_world_size(), "rank_sum": int(t.item()),
+                          "backend": dist.get_backend()}))
+    dist.destroy_process_group()
 
 
 def cpu_model() -> str:
@@ -194,7 +250,7 @@ def cpu_baseline(args):
                       "O0": "-Wall -Wextra -Werror -pedantic -std=c99 -g -fPIC (Justfile:8 CFLAGS)"}}
 
 
-def cpu_leg(args, world, fwd_check, huf_check):
+def cpu_leg(args, world, fwd_check, huf_check, rt_check=None):
     """The CPU leg (rank 0): the reference's own CPU path timed on this host
     (cpu_baseline, N=1 only), and the oracle as CHECKER of this run's GPU
     outputs -- one chroma plane's coefficients and its per-block Huffman sizes.
@@ -210,10 +266,38 @@ def cpu_leg(args, world, fwd_check, huf_check):
         if huf_check is not None:
             c, b = huf_check
             parity["huffman"] = bool(np.array_equal(b.view(np.uint32), O.huffman_bits_plane(c)))
+        if rt_check is not None:
+            parity["round_trip"] = round_trip_parity(args, rt_check)
     except Exception as e:  # noqa: BLE001 -- report, do not hide
         parity["error"] = str(e)
     cpu = cpu_baseline(args) if world == 1 else None
     return cpu, parity
+
+
+def round_trip_parity(args, ck):
+    """The fused round trip's output for chroma frame 0 against the oracle:
+    coefficients bit-exact (forward_plane), recon within 1e-4 of
+    dct_inverse(dequantize()) + 128 (inverse_plane; src/quantization.c:133-151,
+    src/dct.c:80-105), and luma frame 0's PSNR equal to the oracle pipeline's
+    (tests/test_entropy.c:376-393 formula, recon clamped to [0, 255])."""
+    import math
+    import numpy as np
+    import oracle as O
+    q, ad = args.quality, args.adaptive
+    want_c = O.forward_plane(ck["px"], q, ad, 8)
+    var = O.plane_variance(ck["px"]) if ad else None
+    want_r = O.inverse_plane(want_c, q, ad, var) + 128.0
+    err = float(np.abs(ck["recon"].astype(np.float64) - want_r).max())
+    y = ck["luma0"]
+    h, w = y.shape
+    yc = O.forward_plane(y, q, ad, 8)
+    yr = O.inverse_plane(yc, q, ad, O.plane_variance(y) if ad else None) + 128.0
+    blocks = y.reshape(h // 8, 8, w // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64).astype(np.float64)
+    mse = float(((blocks - np.clip(yr, 0, 255)) ** 2).mean())
+    psnr = float("inf") if mse == 0 else 10.0 * math.log10(255.0 * 255.0 / mse)
+    return {"coef_bit_exact": bool(np.array_equal(ck["coef"], want_c)), "recon_max_abs_err": err,
+            "recon_within_1e-4": err <= 1e-4, "psnr_oracle_db": psnr, "psnr_gpu_db": ck["psnr"],
+            "psnr_abs_diff": abs(psnr - ck["psnr"]), "blocks": int(want_c.shape[0])}
 
 
 def band_leg(args, plan, luma, chroma, world, dev, reps=20):
@@ -242,25 +326,29 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
         plan.forward_quant_planes(bands, outs=outs)
         return shard.gather_planes(outs, counts)  # the three planes in one collective
 
-    full = once()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        full = once()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+    def timed(fn):
+        r = fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            r = fn()
+        torch.cuda.synchronize()
+        return shard.max_over_ranks(time.perf_counter() - t0, dev), r
+
+    el, full = timed(once)
+    el_g, _ = timed(lambda: shard.gather_planes(outs, counts))  # the exchange alone
     want = plan.forward_quant_planes(planes)
     ok = all(bool(torch.equal(f, w)) for f, w in zip(full, want))
     nblk = sum(w.shape[0] for w in want)
     be = "RCCL all_gather_into_tensor" if dist.get_backend() == "nccl" else f"{dist.get_backend()} all_gather"
+    rank = dist.get_rank()
+    recv = sum(sum(c) - c[rank] for c in counts) * 128
     return {"op": f"one 4K 4:2:0 frame in block-row bands over {world} ranks: forward_quant_planes(bands) + {be} "
                   "of the Y/Cb/Cr coefficient planes", "frames": reps, "us_per_frame": el / reps * 1e6,
-            "blocks_per_s": nblk * reps / el, "gathered_equals_unsharded": ok}
+            "blocks_per_s": nblk * reps / el, "gathered_equals_unsharded": ok,
+            "xgmi": shard.xgmi_report(recv, el_g / reps, world)}
 
 
 def gather_leg(args, plan, world, rank, dev):
@@ -294,7 +382,8 @@ def gather_leg(args, plan, world, rank, dev):
             "frames_total": args.total_frames, "frames_this_rank": hi - lo, "steps": r["steps"],
             "kernel_blocks_per_s": n / r["kernel_s"], "kernel_ms_per_step": r["kernel_s"] / r["steps"] * 1e3,
             "blocks_per_s": n / r["end_to_end_s"], "ms_per_step": r["end_to_end_s"] / r["steps"] * 1e3,
-            "bytes_received_per_rank": (sum(counts) - counts[rank]) * 128, "own_slice_intact": ok}
+            "bytes_received_per_rank": (sum(counts) - counts[rank]) * 128, "own_slice_intact": ok,
+            "xgmi": shard.xgmi_report((sum(counts) - counts[rank]) * 128, r["gather_s"] / r["steps"], world)}
 
 
 def small_frame_leg(args, plan, dev):
@@ -449,7 +538,7 @@ def encode_leg(args, plan, luma, chroma, world, dev):
     return out
 
 
-def round_trip_leg(args, plan, luma, chroma, world, dev):
+def round_trip_leg(args, plan, luma, chroma, world, rank, dev):
     """BASELINE configs[4]: forward DCT+quant then dequant+IDCT of every plane of
     the frame stream, FUSED (dctq_round_trip_planes: one launch, the quantized
     ints handed to the inverse through LDS, 448 B/block), end-to-end blocks/s
@@ -492,7 +581,7 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
         return el
 
     el_u = timed(unfused)
-    el = timed(fused)  # last: rec holds the fused kernel's output
+    el = timed(fused)  # rec / co hold the fused kernel's output from here on
     nblk = sum(nbs)
     # PSNR of luma frame 0 (block order is raster, so compare block by block)
     h, w = luma.shape[1], luma.shape[2]
@@ -504,6 +593,14 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
         return float("inf") if mse == 0 else 10.0 * math.log10(255.0 * 255.0 / mse)
 
     psnr = psnr_of(rec[0])
+    # host copies for the CPU leg's oracle check (rank 0): chroma frame 0 -- its
+    # pixels, the fused kernel's coefficients and recon -- and luma frame 0's PSNR
+    nk = chroma.shape[1] // 8 * (chroma.shape[2] // 8)
+    check = None
+    if rank == 0:
+        check = {"px": chroma[0].cpu().numpy(), "coef": co[1][:nk].cpu().numpy(), "recon": rec[1][:nk].cpu().numpy(),
+                 "luma0": luma[0].cpu().numpy(), "psnr": psnr}
+    movement = rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev) if args.ceiling_rounds > 0 else None
     # the other dequantization semantics on the same frame: adaptive plans dequantize
     # with Q (src/quantization.c:137,144), non-adaptive ones with the reference's 1/Q
     other = dct_amd.Plan(args.quality, 0 if args.adaptive else 1)
@@ -515,12 +612,62 @@ def round_trip_leg(args, plan, luma, chroma, world, dev):
             "blocks_per_s": world * nblk * args.round_trip_steps / el,
             "ms_per_step": el / args.round_trip_steps * 1e3,
             "bytes_per_block": bpb, "achieved_GBs_per_gpu": nblk * bpb * args.round_trip_steps / el / 1e9,
+            "frac_of_hbm_peak": nblk * bpb * args.round_trip_steps / el / 1e9 / HBM_PEAK_GBS,
+            "movement_ceiling": movement,
             "unfused_blocks_per_s": world * nblk * args.round_trip_steps / el_u,
             "unfused_bytes_per_block": 64 + 128 + 4 + 128 + 4 + 256,
             "psnr_db_luma_frame0": psnr,
             f"psnr_db_luma_frame0_adaptive{0 if args.adaptive else 1}": psnr_other,
             "psnr_note": "adaptive=0 dequantizes with the reference's 1/Q (bug-compatible, src/quantization.c:139,144); "
-                         "adaptive=1 with Q*(2-nv)"}
+                         "adaptive=1 with Q*(2-nv)", "_check": check}
+
+
+def rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev, b2b=3):
+    """Memory ceilings of the fused round trip's traffic (64 B in, 128 + 256 B out
+    per block) on THIS box, in interleaved steady-state rounds beside the fused
+    launch itself (as ceilings_leg does for the forward):
+      movement : dctq_diag_rt_movement_planes -- roundtrip8's exact grid, stage,
+                 prefetch and stores, no arithmetic;
+      flat_124 : dctq_diag_stream 5 -- the same byte counts as a flat persistent
+                 stream (1 KiB loads, 24 x 1 KiB nt stores per 64 blocks).
+    fused_over_own_movement is the kernel's time against its own data movement.
+    Overwrites co/rec (run after the parity copies)."""
+    import statistics
+    D = dct_amd.diag()
+    dplan = dct_amd.Plan(args.quality, args.adaptive, diagnostic=True)
+    nflat = nblk // 64 * 64
+    src = torch.full((nflat * 64,), 7, dtype=torch.uint8, device=dev)
+    dst = torch.empty(nflat * 384, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def flat():
+        rc = D.dctq_diag_stream(5, src.data_ptr(), dst.data_ptr(), nflat, stream)
+        if rc:
+            raise RuntimeError(f"dctq_diag_stream(5) rc={rc}")
+
+    bpb = 64 + 128 + 256
+    cases = {"fused": (lambda: plan.round_trip_planes(pls, outs=co, recons=rec), nblk * bpb),
+             "movement": (lambda: dplan.diag_rt_movement_planes(pls, co, rec), nblk * bpb),
+             "flat_124": (flat, nflat * bpb)}
+    times = {k: [] for k in cases}
+    for r in range(args.ceiling_rounds + 1):
+        for k, (fn, _) in cases.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            fn()
+            e0.record()
+            for _ in range(b2b):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            if r:
+                times[k].append(e0.elapsed_time(e1) * 1e-3 / b2b)
+    med = {k: statistics.median(v) for k, v in times.items()}
+    frac = {k: cases[k][1] / med[k] / 1e9 / HBM_PEAK_GBS for k in cases}
+    del src, dst
+    return {"fused_frac": frac["fused"], "movement_frac": frac["movement"], "flat_124_frac": frac["flat_124"],
+            "fused_over_own_movement": frac["fused"] / frac["movement"],
+            "fused_over_flat_124": frac["fused"] / frac["flat_124"], "rounds": args.ceiling_rounds,
+            "launches_per_sample": b2b, "median_us": {k: v * 1e6 for k, v in med.items()}}
 
 
 def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3):
@@ -621,6 +768,15 @@ def traffic_for(args, launches):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))  # one child process per GPU; this process stays off the GPU
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ.get('WORLD_SIZE')} "
+                 "ranks")
+    if args.launch_check:
+        return launch_check(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -735,16 +891,22 @@ def main():
 
     round_trip = None
     if args.round_trip_steps > 0:
-        round_trip = round_trip_leg(args, plan, luma, chroma, world, dev)
+        round_trip = round_trip_leg(args, plan, luma, chroma, world, rank, dev)
 
     total_blocks = world * (nblk_y + nblk_c) * args.steps
     value = total_blocks / el
     traffic, traffic_note = traffic_for(args, launches)
     if rank == 0:
         huf_check = encode["huffman"].pop("_check", None) if encode else None
-        cpu, parity = (None, None) if args.no_cpu else cpu_leg(args, world, fwd_check, huf_check)
+        rt_check = round_trip.pop("_check", None) if round_trip else None
+        cpu, parity = (None, None) if args.no_cpu else cpu_leg(args, world, fwd_check, huf_check, rt_check)
         if encode and parity is not None:
             encode["huffman"]["parity_check_chroma0"] = parity.get("huffman")
+        if round_trip and parity is not None and "round_trip" in parity:
+            rp = parity["round_trip"]
+            round_trip["parity"] = rp
+            round_trip["parity_check"] = bool(rp["coef_bit_exact"] and rp["recon_within_1e-4"]
+                                              and rp["psnr_abs_diff"] <= 1e-3)
         out = {
             "metric": "8x8 macroblocks/sec (DCT+quant); % HBM roofline",
             "value": value,
@@ -763,7 +925,7 @@ def main():
                                    f"forward DCT+quant q{args.quality} adaptive={args.adaptive}, int16 out",
                        "frames_per_gpu": F, "blocks_per_gpu_step": nblk_y + nblk_c, "quality": args.quality,
                        "adaptive": args.adaptive, "parallelism": f"frames sharded over {world} GPU(s)",
-                       "world_size": world},
+                       "world_size": world, "backend": dist.get_backend() if dist_on else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
                          "kernel": f"fdct8_quant_v2<{bool(args.adaptive)}, false, false>".lower(),
@@ -771,6 +933,7 @@ def main():
                          "bytes_per_launch": avg_launch_bytes, "movement_ceiling": movement},
             "cpu_baseline": cpu,
             "parity_check": parity.get("forward") if parity else None,
+            "parity_error": parity.get("error") if parity else None,
             "gather": gather,
             "band": band,
             "round_trip": round_trip,

@@ -62,6 +62,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
         sig.update({
             "dctq_diag_plan_set_variant": ([vp, i], i),
             "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
+            "dctq_diag_rt_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_diag_stream": ([i, vp, vp, ll, vp], i),
             "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
             "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
@@ -101,6 +102,24 @@ def _check(rc: int, L: C.CDLL = None) -> None:
         raise DctqError(f"dctq error {rc}: {(L or lib()).dctq_error_string(rc).decode()}")
 
 
+def _need(t, numel: int, dtype, what: str, device=None):
+    """A caller-supplied buffer must be a contiguous device tensor of the right
+    dtype holding at least `numel` elements (on `device` when given): the kernels
+    write through the raw pointer, so a short or host tensor is refused here."""
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise DctqError(f"{what} must be a tensor on a HIP device")
+    if t.dtype != dtype:
+        raise DctqError(f"{what} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise DctqError(f"{what} must be contiguous")
+    if t.numel() < numel:
+        raise DctqError(f"{what} holds {t.numel()} elements, {numel} needed")
+    if device is not None and t.device != device:
+        raise DctqError(f"{what} is on {t.device}, the input is on {device}")
+    return t
+
+
 def _stream_ptr(stream=None):
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
@@ -119,6 +138,20 @@ def plane_desc(px, width: int = None, height: int = None):
     f, h, w = px.shape
     return _Plane(px.data_ptr(), px.stride(1), px.stride(0) if f > 1 else px.stride(1) * h,
                   width if width is not None else w, height if height is not None else h, f)
+
+
+def _need_planes(outs, var_nums, recons, nbs, planes):
+    """Per-plane output lists of the multi-plane calls: one entry per plane, each
+    sized for that plane's blocks (_need)."""
+    import torch
+    for name, ts, per, dt in (("outs", outs, 64, torch.int16), ("var_nums", var_nums, 1, torch.int32),
+                              ("recons", recons, 64, torch.float32)):
+        if ts is None:
+            continue
+        if len(ts) != len(nbs):
+            raise DctqError(f"{name} needs one tensor per plane ({len(nbs)}), got {len(ts)}")
+        for k, (t, nb, px) in enumerate(zip(ts, nbs, planes)):
+            _need(t, nb * per, dt, f"{name}[{k}]", px.device)
 
 
 class Plan:
@@ -164,6 +197,9 @@ class Plan:
         nblk = d.nframes * (d.width // 8) * (d.height // 8)
         if out is None:
             out = torch.empty((nblk, 64), dtype=torch.int16, device=px.device)
+        _need(out, nblk * 64, torch.int16, "out", px.device)
+        if var_num is not None:
+            _need(var_num, nblk, torch.int32, "var_num", px.device)
         self._chk(self._L.dctq_forward_quant(self._h, C.byref(d), C.c_void_p(out.data_ptr()),
                                         C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
                                         _stream_ptr(stream)))
@@ -175,9 +211,10 @@ class Plan:
         import torch
         n = len(planes)
         descs = (_Plane * n)(*[plane_desc(px) for px in planes])
+        nbs = [d.nframes * (d.width // 8) * (d.height // 8) for d in descs]
         if outs is None:
-            outs = [torch.empty((d.nframes * (d.width // 8) * (d.height // 8), 64), dtype=torch.int16,
-                                device=px.device) for d, px in zip(descs, planes)]
+            outs = [torch.empty((nb, 64), dtype=torch.int16, device=px.device) for nb, px in zip(nbs, planes)]
+        _need_planes(outs, var_nums, None, nbs, planes)
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         vp = (C.c_void_p * n)(*[v.data_ptr() for v in var_nums]) if var_nums is not None else None
         self._chk(self._L.dctq_forward_quant_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
@@ -190,11 +227,27 @@ class Plan:
         pixel bytes, not coefficients) -- the memory ceiling of that access pattern."""
         n = len(planes)
         descs = (_Plane * n)(*[plane_desc(px) for px in planes])
+        _need_planes(outs, None, None, [d.nframes * (d.width // 8) * (d.height // 8) for d in descs], planes)
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         if self._L is not _diag:
             raise DctqError("diag_movement_planes needs a plan of the diagnostic library (Plan(..., diagnostic=True))")
         self._chk(self._L.dctq_diag_movement_planes(self._h, descs, n, C.cast(cp, C.c_void_p), _stream_ptr(stream)))
         return outs
+
+    def diag_rt_movement_planes(self, planes, outs, recons, stream=None):
+        """DIAGNOSTIC: the bytes round_trip_planes moves (its grid, stage and stores), with no
+        arithmetic (outs/recons receive pixel bytes) -- the memory ceiling of that pattern."""
+        n = len(planes)
+        descs = (_Plane * n)(*[plane_desc(px) for px in planes])
+        nbs = [d.nframes * (d.width // 8) * (d.height // 8) for d in descs]
+        _need_planes(outs, None, recons, nbs, planes)
+        if self._L is not _diag:
+            raise DctqError("diag_rt_movement_planes needs a plan of the diagnostic library (Plan(..., diagnostic=True))")
+        cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+        rp = (C.c_void_p * n)(*[r.data_ptr() for r in recons])
+        self._chk(self._L.dctq_diag_rt_movement_planes(self._h, descs, n, C.cast(cp, C.c_void_p), C.cast(rp, C.c_void_p),
+                                                      _stream_ptr(stream)))
+        return outs, recons
 
     def round_trip_planes(self, planes, outs=None, recons=None, var_nums=None, stream=None):
         """Fused forward + inverse of up to 4 planes in ONE launch.  Returns (coefs, recons):
@@ -208,6 +261,7 @@ class Plan:
             outs = [torch.empty((nb, 64), dtype=torch.int16, device=px.device) for nb, px in zip(nbs, planes)]
         if recons is None:
             recons = [torch.empty((nb, 64), dtype=torch.float32, device=px.device) for nb, px in zip(nbs, planes)]
+        _need_planes(outs, var_nums, recons, nbs, planes)
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         rp = (C.c_void_p * n)(*[r.data_ptr() for r in recons])
         vp = (C.c_void_p * n)(*[v.data_ptr() for v in var_nums]) if var_nums is not None else None
@@ -229,6 +283,7 @@ class Plan:
         dev = planes[0].device
         if outs is None:
             outs = [torch.empty((m, 64), dtype=torch.int16, device=dev) for m in nbs]
+        _need_planes(outs, None, None, nbs, planes)
         cap = 64 * nb if capacity is None else int(capacity)
         off = torch.empty(nb + 1, dtype=torch.int32, device=dev)
         sym = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
@@ -250,6 +305,7 @@ class Plan:
         nb = sum(d.nframes * (d.width // 8) * (d.height // 8) for d in descs)
         if out is None:
             out = torch.empty(nb, dtype=torch.int32, device=planes[0].device)
+        _need(out, nb, torch.int32, "out", planes[0].device)
         self._chk(self._L.dctq_huffman_bits_planes(self._h, descs, n, C.c_void_p(out.data_ptr()),
                                                    _stream_ptr(stream)))
         return out
@@ -260,15 +316,20 @@ class Plan:
         nblk = d.nframes * (d.width // 8) * (d.height // 8)
         if out is None:
             out = torch.empty((nblk, 64), dtype=torch.float32, device=px.device)
+        _need(out, nblk * 64, torch.float32, "out", px.device)
         self._chk(self._L.dctq_forward_float(self._h, C.byref(d), C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
         return out
 
     def inverse(self, coef, var_num=None, out=None, stream=None):
         """int16 [N, 64] -> float32 [N, 64] = dct_inverse(dequantize(coef)) + 128."""
         import torch
+        _need(coef, 0, torch.int16, "coef")
         n = coef.numel() // 64
         if out is None:
             out = torch.empty((n, 64), dtype=torch.float32, device=coef.device)
+        _need(out, n * 64, torch.float32, "out", coef.device)
+        if var_num is not None:
+            _need(var_num, n, torch.int32, "var_num", coef.device)
         self._chk(self._L.dctq_inverse(self._h, C.c_void_p(coef.data_ptr()),
                                   C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
                                   n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
@@ -280,6 +341,7 @@ def rle_encode(coef, stream=None):
     block, concatenated).  Returns (offsets [N+1], symbols [total]) as int32 tensors holding the
     uint32 bit patterns: symbol = (uint16)value | run << 16.  Reads the total back (one sync)."""
     import torch
+    _need(coef, 0, torch.int16, "coef")
     n = coef.numel() // 64
     ws = torch.empty(int(lib().dctq_rle_workspace_bytes(n)) // 4 + 1, dtype=torch.int32, device=coef.device)
     off = torch.empty(n + 1, dtype=torch.int32, device=coef.device)
@@ -298,9 +360,11 @@ def huffman_bits(coef, out=None, stream=None):
     get_encoded_size reports after build_huffman_codes on that block's RLE symbols
     (tests/test_entropy.c:329-341)."""
     import torch
-    n = coef.shape[0]
+    _need(coef, 0, torch.int16, "coef")
+    n = coef.numel() // 64
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=coef.device)
+    _need(out, n, torch.int32, "out", coef.device)
     _check(lib().dctq_huffman_bits(C.c_void_p(coef.data_ptr()), n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
     return out
 
@@ -311,6 +375,7 @@ def rle_decode(symbols, offsets, out=None, stream=None):
     n = offsets.numel() - 1
     if out is None:
         out = torch.empty((n, 64), dtype=torch.int16, device=offsets.device)
+    _need(out, n * 64, torch.int16, "out", offsets.device)
     _check(lib().dctq_rle_decode(C.c_void_p(symbols.data_ptr()), C.c_void_p(offsets.data_ptr()), n,
                                  C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
     return out

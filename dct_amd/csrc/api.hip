@@ -10,8 +10,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <string>
+#include <utility>
 
 #include "dct_amd.h"
 #include "dctq_internal.h"
@@ -136,13 +138,6 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
         delete p;
         return fail(DCTQ_EHIP, "hipMemcpy(plan tables)", e);
     }
-    p->ring_wgs = dctq::fdct8_ring_workgroups(p->num_cus);  // the v2 grid's workgroups
-    e = hipMalloc(&p->ring, dctq::fdct8_ring_bytes(p->ring_wgs));
-    if (e != hipSuccess) {
-        (void)hipFree(p->dev);
-        delete p;
-        return fail(DCTQ_ENOMEM, "hipMalloc(tie-path stash)", e);
-    }
     *out = p;
     return DCTQ_OK;
 }
@@ -219,7 +214,6 @@ void dctq_plan_destroy(dctq_plan *plan) {
     DCTQ_ENTRY;
     if (!plan) return;
     (void)hipFree(plan->dev);
-    (void)hipFree(plan->ring);
     delete plan;
 }
 
@@ -241,22 +235,16 @@ int dctq::check_plan(const dctq_plan *plan) {
     return DCTQ_OK;
 }
 
-int dctq::plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num,
-                    dctq::PlaneSet *ps_out) {
-    if (!planes || !coef) return fail(DCTQ_EINVAL, "planes/coef is NULL");
+int dctq::plane_inputs(const dctq_plane *planes, int nplanes, dctq::PlaneSet *ps_out) {
+    if (!planes) return fail(DCTQ_EINVAL, "planes is NULL");
     if (nplanes < 1 || nplanes > dctq::kMaxPlanes) return fail(DCTQ_EINVAL, "nplanes must be in [1, 4]");
     dctq::PlaneSet &ps = *ps_out;
     ps = {};
     ps.n = nplanes;
     uint32_t first = 0;
     for (int k = 0; k < nplanes; ++k) {
-        if (!coef[k]) return fail(DCTQ_EINVAL, "coef[k] is NULL");
-        if (((uintptr_t)coef[k]) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
-        if (var_num && !var_num[k]) return fail(DCTQ_EINVAL, "var_num given but var_num[k] is NULL");
         int rc = dctq::plane_args(&planes[k], &ps.pl[k]);
         if (rc) return rc;
-        ps.coef[k] = coef[k];
-        ps.var[k] = var_num ? var_num[k] : nullptr;
         ps.first[k] = first;
         first += (uint32_t)((ps.pl[k].nblk + 63) / 64);  // < 4 * 2^25
     }
@@ -264,6 +252,65 @@ int dctq::plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef,
     for (int k = nplanes + 1; k <= dctq::kMaxPlanes; ++k) ps.first[k] = first;
     return DCTQ_OK;
 }
+
+int dctq::plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num,
+                    dctq::PlaneSet *ps_out) {
+    if (!planes || !coef) return fail(DCTQ_EINVAL, "planes/coef is NULL");
+    if (int rc = dctq::plane_inputs(planes, nplanes, ps_out)) return rc;
+    dctq::PlaneSet &ps = *ps_out;
+    for (int k = 0; k < nplanes; ++k) {
+        if (!coef[k]) return fail(DCTQ_EINVAL, "coef[k] is NULL");
+        if (((uintptr_t)coef[k]) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
+        if (var_num && !var_num[k]) return fail(DCTQ_EINVAL, "var_num given but var_num[k] is NULL");
+        ps.coef[k] = coef[k];
+        ps.var[k] = var_num ? var_num[k] : nullptr;
+    }
+    return DCTQ_OK;
+}
+
+// The v2 forward's tie-path pixel stash (fdct8.hip: 8 KiB per wave of the
+// launched grid).  One per (device, stream), allocated on the first launch that
+// needs it and grown to the largest grid launched there: launches on one stream
+// run in order, so every plan used on that stream shares it, and a plan costs
+// no stash at all until it runs a multi-batch-per-wave forward.  The mutex is
+// held from the lookup to the kernel launch (stash_guard), so a grow -- which
+// waits for the stream before freeing the smaller stash -- never frees memory a
+// launch enqueued by another thread is about to use.
+namespace {
+struct Stash {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+};
+std::mutex g_stash_mu;
+std::map<std::pair<int, hipStream_t>, Stash> g_stash;
+struct StashCtx {
+    int device;
+    hipStream_t stream;
+    hipError_t err;
+};
+
+void *stash_for(void *vctx, size_t bytes) {  // called with g_stash_mu held
+    StashCtx &c = *static_cast<StashCtx *>(vctx);
+    Stash &s = g_stash[{c.device, c.stream}];
+    if (s.bytes >= bytes) return s.ptr;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(c.stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
+        c.err = hipErrorStreamCaptureUnsupported;  // run the launch once before capturing it
+        return nullptr;
+    }
+    if (s.ptr) {
+        if ((c.err = hipStreamSynchronize(c.stream)) != hipSuccess) return nullptr;
+        (void)hipFree(s.ptr);
+        s = Stash{};
+    }
+    if ((c.err = hipMalloc(&s.ptr, bytes)) != hipSuccess) {
+        s = Stash{};
+        return nullptr;
+    }
+    s.bytes = bytes;
+    return s.ptr;
+}
+}  // namespace
 
 extern "C" {
 
@@ -274,9 +321,18 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
     dctq::PlaneSet ps;
     int rc = dctq::plane_set(planes, nplanes, coef, var_num, &ps);
     if (rc) return rc;
-    HIPCHK(dctq::launch_fdct8_quant(ps, plan->fast, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
-                                    plan->variant, plan->num_cus, plan->ring, plan->ring_wgs),
-           "fdct8_quant launch");
+    StashCtx sc{plan->device, (hipStream_t)stream, hipSuccess};
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> stash_guard(g_stash_mu);
+        e = dctq::launch_fdct8_quant(ps, plan->fast, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
+                                     plan->variant, plan->num_cus, dctq::RingSource{stash_for, &sc});
+    }
+    if (sc.err == hipErrorStreamCaptureUnsupported)
+        return fail(DCTQ_EINVAL, "the tie-path stash of this stream is smaller than this launch needs: run the launch "
+                                 "once on the stream before capturing it");
+    if (sc.err != hipSuccess) return fail(DCTQ_ENOMEM, "tie-path stash", sc.err);
+    HIPCHK(e, "fdct8_quant launch");
     return DCTQ_OK;
 }
 
@@ -436,10 +492,9 @@ int dctq_huffman_bits_planes(const dctq_plan *plan, const dctq_plane *planes, in
     DCTQ_ENTRY;
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!bits || ((uintptr_t)bits) % 4) return fail(DCTQ_EINVAL, "bits is NULL or not 4-byte aligned");
-    // plane_set's coefficient pointers are not used by this launch (they stay on chip)
-    int16_t *const none[dctq::kMaxPlanes] = {(int16_t *)16, (int16_t *)16, (int16_t *)16, (int16_t *)16};
+    // pixel planes only: the coefficients stay on chip (es.ps.coef stays NULL)
     dctq::EncodeSet es = {};
-    int rc = dctq::plane_set(planes, nplanes, none, nullptr, &es.ps);
+    int rc = dctq::plane_inputs(planes, nplanes, &es.ps);
     if (rc) return rc;
     long long blocks = 0;
     for (int k = 0; k < nplanes; ++k) {

@@ -26,6 +26,11 @@ int dctq_diag_plan_set_variant(dctq_plan *plan, int variant);
 int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               void *stream);
 
+/* The same for the fused round trip (dctq_round_trip_planes): its grid, stage
+ * and stores with no arithmetic; coef[k] and recon[k] receive pixel bytes. */
+int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                 float *const *recon, void *stream);
+
 /* Hardware ceilings of the forward kernel's traffic (64 B read : 128 B written
  * per block), independent of its access pattern (profiles/r02/hbm_ceilings.md):
  *   kind 0: flat 1:2 stream, per wave 4 x 1 KiB loads then 8 x 1 KiB stores per
@@ -33,8 +38,11 @@ int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, i
  *   kind 1: the same with default-policy stores;
  *   kind 2: read-only stream of blocks * 64 bytes of src (nt);
  *   kind 3: write-only stream of blocks * 128 bytes of dst (default policy);
- *   kind 4: the same with non-temporal stores.
- * src >= blocks * 64 bytes, dst >= blocks * 128 bytes, both 16-byte aligned. */
+ *   kind 4: the same with non-temporal stores;
+ *   kind 5: the round trip's mix, flat: 64 B read : 128 + 256 B written per
+ *           block (per wave 4 x 1 KiB loads, 24 x 1 KiB nt stores), persistent.
+ * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kind 5: blocks * 384),
+ * both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
 
 /* Host-only introspection for the CPU tests (no GPU needed). */

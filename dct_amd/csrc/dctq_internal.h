@@ -40,7 +40,7 @@ inline int resident_per_cu(K kernel, int threads) {
 // retires, which evens out batches of unequal cost and the launch tail
 // (profiles/r02/grid_mult_ab.log: x8 is 2.4-7 % faster than x1 on the forward,
 // round trip, inverse and encoder, outputs identical; x16/x32 regress on
-// uniform input).  The forward's stash ring is sized for this grid.
+// uniform input).  The forward's stash is sized for the grid it launches.
 // Cache policy of the bulk 1 KiB output stores of every streaming kernel
 // (buffer-store aux bits, gfx950: 1 sc0, 2 nt, 16 sc1).  Non-temporal: the
 // written lines are never re-read by the kernel that writes them.
@@ -118,16 +118,24 @@ struct RoundTripSet {
     float *recon[kMaxPlanes];
 };
 
+// Where the v2 forward gets its tie-path pixel stash: get(ctx, bytes) returns
+// device memory of at least `bytes` that no other in-flight launch uses, or
+// nullptr (api.hip: one stash per (device, stream), grown to the launched grid).
+struct RingSource {
+    void *(*get)(void *ctx, size_t bytes);
+    void *ctx;
+};
 hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
-                              unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus, void *ring,
-                              int ring_wgs);
+                              unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus,
+                              const RingSource &ring);
 // bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
 size_t fdct8_ring_bytes(int workgroups);
-int fdct8_ring_workgroups(int num_cus);
 // diagnostic: fdct8_quant_v2's data movement without arithmetic (fdct8.hip)
 hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num_cus);
 hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
                             hipStream_t stream, int num_cus);
+// diagnostic: roundtrip8's data movement without arithmetic (roundtrip.hip)
+hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream, int num_cus);
 size_t encode_workspace_bytes(long long nbatch);
 hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *offsets,
                          uint32_t *symbols, unsigned long long capacity, void *ws, hipStream_t stream, int num_cus);

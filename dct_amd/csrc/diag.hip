@@ -33,6 +33,25 @@ __global__ __launch_bounds__(256) void stream12(const u4v *__restrict__ src, cha
     }
 }
 
+// Flat 1:2:4 stream (the fused round trip's 64 B in : 128 + 256 B out): wave-batch
+// b reads src[4 KiB * b, +4 KiB) and writes dst[24 KiB * b, +24 KiB), nt stores.
+__global__ __launch_bounds__(256) void stream124(const u4v *__restrict__ src, char *__restrict__ dst, uint32_t nb) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < nb; b += gridDim.x * 4) {
+        u4v v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(src + (size_t)b * 256 + k * 64 + lane);
+        const __amdgpu_buffer_rsrc_t rc =
+            __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 24576, 0, 24576, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int m = 0; m < 6; ++m)
+                __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)m, 0, 0, 0}, rc, lane * 16,
+                                                       (k * 6 + m) * 1024, 2);
+    }
+}
+
 // read-only: 4 x 16 B per thread, xor-reduced (the store never happens)
 __global__ __launch_bounds__(256) void stream_read(const u4v *__restrict__ src, u4v *__restrict__ sink, size_t n16) {
     const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
@@ -85,6 +104,21 @@ int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, i
     return DCTQ_OK;
 }
 
+int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                 float *const *recon, void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = dctq::check_plan(plan)) return rc;
+    if (!recon) return dctq::fail(DCTQ_EINVAL, "recon is NULL");
+    dctq::RoundTripSet rt = {};
+    if (int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &rt.ps)) return rc;
+    for (int k = 0; k < nplanes; ++k) {
+        if (!recon[k] || ((uintptr_t)recon[k]) % 16) return dctq::fail(DCTQ_EINVAL, "recon[k] NULL or misaligned");
+        rt.recon[k] = recon[k];
+    }
+    HIPCHK(dctq::launch_roundtrip_movement(rt, (hipStream_t)stream, plan->num_cus), "roundtrip_movement launch");
+    return DCTQ_OK;
+}
+
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream) {
     DCTQ_ENTRY;
     using namespace dctq;
@@ -111,7 +145,8 @@ int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, voi
             hipLaunchKernelGGL(stream_write<true>, dim3((unsigned)((n16 + 1023) / 1024)), dim3(256), 0, s, (u4v *)dst, n16);
         break;
     }
-    default: return fail(DCTQ_EINVAL, "kind must be 0..4");
+    case 5: hipLaunchKernelGGL(stream124, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
+    default: return fail(DCTQ_EINVAL, "kind must be 0..5");
     }
     HIPCHK(hipGetLastError(), "diag stream launch");
     return DCTQ_OK;

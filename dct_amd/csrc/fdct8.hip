@@ -465,14 +465,18 @@ static hipError_t launch_v1(const PlaneSet &ps, const FastTables &t, const DevTa
 
 template <bool A, bool V, bool S>
 static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTables *dev, unsigned long long *fb,
-                            hipStream_t stream, int num_cus, void *ring, int ring_wgs) {
+                            hipStream_t stream, int num_cus, const RingSource &rs) {
     static const int per_cu = resident_per_cu(fdct8_quant_v2<A, V, S>, kFThreads);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
-    uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
-    if (cap > (uint32_t)ring_wgs) cap = (uint32_t)ring_wgs;
-    hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps, t, dev,
-                       fb, (uint4 *)ring);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
+    const uint32_t grid = want < cap ? want : cap;
+    // the stash is sized to THIS grid (every workgroup owns its waves' slots) and
+    // handed out by the caller per (device, stream): launches on one stream are
+    // ordered, so they share it (api.hip stash_for)
+    void *ring = rs.get(rs.ctx, fdct8_ring_bytes((int)grid));
+    if (!ring) return hipErrorOutOfMemory;
+    hipLaunchKernelGGL((fdct8_quant_v2<A, V, S>), dim3(grid), dim3(kFThreads), 0, stream, ps, t, dev, fb, (uint4 *)ring);
     return hipGetLastError();
 }
 
@@ -549,20 +553,18 @@ static hipError_t launch_v3(const PlaneSet &ps, const DevTables *dev, unsigned l
 }
 
 size_t fdct8_ring_bytes(int workgroups) { return (size_t)workgroups * kFWaves * kQCap * 64; }
-// Workgroups the stash ring serves: the resident ones (16 waves per CU: 4 per SIMD, VGPR-bound) times the
-// grid multiplier.
-int fdct8_ring_workgroups(int num_cus) { return num_cus * (16 / kFWaves) * DCTQ_GRID_MULT; }
 
 hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
-                              unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus, void *ring,
-                              int ring_wgs) {
+                              unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus,
+                              const RingSource &ring) {
     const bool a = adaptive != 0, v = ps.var[0] != nullptr, s = fallbacks != nullptr;
     if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
-    // at most one batch per wave of the resident grid: in-place ties (no drain tail)
-    const bool single = ps.first[ps.n] <= (uint32_t)(ring_wgs / DCTQ_GRID_MULT) * kFWaves;
+    // at most one batch per wave of the resident grid (16 waves per CU: 4 per SIMD,
+    // VGPR-bound): in-place ties, no stash and no drain tail
+    const bool single = ps.first[ps.n] <= (uint32_t)(num_cus * 16);
     if (variant == 3 || (variant == 2 && single))  // variant 4: the queue kernel at any size (A/B)
         DCTQ_SELECT(return launch_v3, a, v, s, (ps, dev, fallbacks, stream, num_cus));
-    DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring, ring_wgs));
+    DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring));
 }
 
 // ============================================================================

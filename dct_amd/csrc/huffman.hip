@@ -590,6 +590,9 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
 #ifndef DCTQ_HP_PREFETCH
 #define DCTQ_HP_PREFETCH 0  // A/B: huffman_from_pixels prefetches the next batch's rows into registers
 #endif
+#if DCTQ_HP_PREFETCH && DCTQ_HP_DIRECT
+#error "DCTQ_HP_PREFETCH is only wired into the tile-layout path (DCTQ_HP_DIRECT=0): the direct path never refreshes the prefetched rows"
+#endif
 #ifndef DCTQ_HUF_MIN_WAVES
 #define DCTQ_HUF_MIN_WAVES 3
 #endif

@@ -154,10 +154,11 @@ __global__ void k_variance(int nn, const double *__restrict__ x, double *__restr
 // arrays into it, launches a kernel that reads its inputs from it and writes its
 // outputs back into it over the host link, and synchronizes: no memcpy calls.
 // Larger blocks go through a device scratch buffer instead (copied once each
-// way).  One buffer of each for the process: every entry point holds the
-// library-wide entry lock (DCTQ_ENTRY), so calls never overlap, and a thread
-// that exits leaves nothing behind.  Both are grown on demand and kept for the
-// life of the process (their memory goes back with it).
+// way).  One buffer of each per device (the current one at the call: a host may
+// switch devices between calls): every entry point holds the library-wide entry
+// lock (DCTQ_ENTRY), so calls never overlap, and a thread that exits leaves
+// nothing behind.  Both are grown on demand and kept for the life of the
+// process (their memory goes back with it).
 struct Staging {
     unsigned char *host = nullptr;  // pinned host memory
     unsigned char *dev = nullptr;   // the same pages as seen by the device
@@ -186,8 +187,17 @@ struct Scratch {
         return dev;
     }
 };
-Staging g_stage;
-Scratch g_scratch;
+constexpr int kMaxDevices = 64;
+Staging g_stages[kMaxDevices];
+Scratch g_scratches[kMaxDevices];
+int current_device() {
+    int d = 0;
+    LCHK(hipGetDevice(&d), "hipGetDevice");
+    if (d < 0 || d >= kMaxDevices) die("device index out of range");
+    return d;
+}
+Staging &stage_buf() { return g_stages[current_device()]; }
+Scratch &scratch_buf() { return g_scratches[current_device()]; }
 
 void finish(const char *what) {
     LCHK(hipGetLastError(), what);
@@ -211,8 +221,9 @@ void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
     check_n(n);
     const size_t nn = (size_t)n * n;
     if (4 * nn * sizeof(double) <= (size_t)kLdsBytes) {
-        double *h = (double *)g_stage.get(sizeof(double) * 4 * nn);
-        const double *dv = (const double *)g_stage.dev;
+        Staging &sg = stage_buf();
+        double *h = (double *)sg.get(sizeof(double) * 4 * nn);
+        const double *dv = (const double *)sg.dev;
         pack(ctx->dct_matrix, n, h);
         pack(ctx->transposed_dct, n, h + nn);
         pack(input, n, h + 2 * nn);
@@ -233,7 +244,7 @@ void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
     pack(ctx->dct_matrix, n, h.data());
     pack(ctx->transposed_dct, n, h.data() + nn);
     pack(input, n, h.data() + 2 * nn);
-    double *d = (double *)g_scratch.get(sizeof(double) * 5 * nn), *t = d + nn, *in = d + 2 * nn, *tmp = d + 3 * nn,
+    double *d = (double *)scratch_buf().get(sizeof(double) * 5 * nn), *t = d + nn, *in = d + 2 * nn, *tmp = d + 3 * nn,
            *out = d + 4 * nn;
     LCHK(hipMemcpy(d, h.data(), sizeof(double) * 3 * nn, hipMemcpyHostToDevice), "hipMemcpy(legacy transform in)");
     const unsigned grid = (unsigned)((nn + 255) / 256);
@@ -255,13 +266,14 @@ void elementwise(int mode, int n, double **m, int flag, double variance, const d
     DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int nn = n * n;
     const size_t bytes = sizeof(double) * 3 * (size_t)nn + sizeof(int) * 2 * (size_t)nn;
-    unsigned char *h = g_stage.get(bytes);
+    Staging &sg = stage_buf();
+    unsigned char *h = sg.get(bytes);
     double *hm = (double *)h, *hd = hm + nn;
     int *hi = (int *)(hd + 2 * nn);
     pack(m, n, hm);
     if (din) memcpy(hd, din, sizeof(double) * nn);
     if (iin) memcpy(hi, iin, sizeof(int) * nn);
-    double *dm = (double *)g_stage.dev, *dd = dm + nn, *ddo = dd + nn;
+    double *dm = (double *)sg.dev, *dd = dm + nn, *ddo = dd + nn;
     int *di = (int *)(ddo + nn), *dio = di + nn;
     hipLaunchKernelGGL(k_elementwise, dim3((nn + 255) / 256), dim3(256), 0, 0, mode, nn, dm, flag, variance, dd, di,
                        ddo, dio);
@@ -417,8 +429,9 @@ double calculate_block_variance(double **block, int block_size) {
     check_n(block_size);
     const size_t nn = (size_t)block_size * block_size;
     if (nn * sizeof(double) <= (size_t)kLdsBytes) {
-        double *hs = (double *)g_stage.get(sizeof(double) * (nn + 1));
-        double *dv = (double *)g_stage.dev;
+        Staging &sg = stage_buf();
+        double *hs = (double *)sg.get(sizeof(double) * (nn + 1));
+        double *dv = (double *)sg.dev;
         pack(block, block_size, hs);
         const int threads = nn < 256 ? (int)((nn + 63) / 64) * 64 : 256;
         hipLaunchKernelGGL(k_variance_small, dim3(1), dim3(threads), sizeof(double) * nn, 0, (int)nn, dv, dv + nn);
@@ -427,7 +440,7 @@ double calculate_block_variance(double **block, int block_size) {
     }
     std::vector<double> h(nn);
     pack(block, block_size, h.data());
-    double *dv = (double *)g_scratch.get(sizeof(double) * (nn + 1));
+    double *dv = (double *)scratch_buf().get(sizeof(double) * (nn + 1));
     LCHK(hipMemcpy(dv, h.data(), sizeof(double) * nn, hipMemcpyHostToDevice), "hipMemcpy(variance in)");
     hipLaunchKernelGGL(k_variance, dim3(1), dim3(1), 0, 0, (int)nn, dv, dv + nn);
     LCHK(hipGetLastError(), "variance launch");

@@ -13,8 +13,6 @@ struct dctq_plan {
     dctq::DevTables host;        // host copy of the device tables
     dctq::DevTables *dev;        // device copy
     unsigned long long *fallbacks;
-    void *ring;                  // v2 tie-path pixel stash (one stream at a time per plan)
-    int ring_wgs;                // workgroups the stash is sized for
 };
 
 namespace dctq {
@@ -22,6 +20,9 @@ namespace dctq {
 int fail(int code, const char *what, hipError_t e = hipSuccess);
 int check_plan(const dctq_plan *plan);
 int plane_args(const dctq_plane *s, PlaneArgs *a);
+// validates the pixel planes and fills ps (batch prefixes); no outputs
+int plane_inputs(const dctq_plane *planes, int nplanes, PlaneSet *ps);
+// plane_inputs plus the per-plane coefficient (and optional var_num) outputs
 int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32_t *const *var_num, PlaneSet *ps);
 void fill_fast_tables(const double *q, int adaptive, FastTables *t);
 // quantized DC of every constant block, in the reference's operation order (api.hip)

@@ -195,6 +195,85 @@ static hipError_t launch_rt(const RoundTripSet &rt, const DevTables *dev, unsign
     return hipGetLastError();
 }
 
+// ============================================================================
+// Diagnostic: roundtrip8's data movement with no arithmetic -- the memory
+// ceiling of this exact access pattern (bench.py round_trip.movement_ceiling).
+// Same grid, occupancy bound, LDS footprint, prefetch, retire/sync points and
+// stores as roundtrip8: per batch the pixel rows go into the stage as the
+// "coefficients" (8 x 1 KiB stores), then twice 32 blocks of 256 B "recon"
+// (the rows repeated) through the paired-inverse stage layout (8 x 1 KiB each).
+__global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(RoundTripSet rt) {
+    __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ ExactTables tabpad;          // same LDS footprint as roundtrip8
+    __shared__ uint16_t scrpad[kWaves * 64];
+    const PlaneSet &ps = rt.ps;
+    if (ps.n < 0) {  // keep the padding allocated
+        scrpad[threadIdx.x] = 0;
+        reinterpret_cast<volatile uint32_t *>(&tabpad)[threadIdx.x] = 0;
+    }
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, j = lane & 31;
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t step = gridDim.x * kWaves;
+    uint32_t g = blockIdx.x * kWaves + wv;
+    uint2 nxt[8];
+    prefetch_batch(ps, g, lane, nxt);
+    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    char *wstage = reinterpret_cast<char *>(stage) + wv * 64 * kPitch2;
+    for (; g < nbatch; g += step) {
+        const int k = plane_of(ps, g);
+        const PlaneArgs &p = ps.pl[k];
+        const uint32_t b = g - ps.first[k];
+        uint2 cur[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+        prefetch_batch<false>(ps, g + step, lane, nxt);
+        uint2 *mine2 = reinterpret_cast<uint2 *>(wstage + lane * kPitch2);
+        retire_stores();
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            mine2[2 * r] = cur[r];
+            mine2[2 * r + 1] = make_uint2(cur[r].y, cur[r].x);
+        }
+        wave_sync();
+        const uint32_t left = (uint32_t)p.nblk - b * 64;
+        const uint32_t nb = left < 64u ? left : 64u;
+        u4v val[8];
+        stage_chunks(stage, wv, lane, val);
+        {
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
+        }
+        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
+        char *mine = wstage + j * kPitchP + h * 128;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            retire_stores();
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                *reinterpret_cast<uint4 *>(mine + r * 16) =
+                    make_uint4(cur[r].x, cur[r].y, cur[r].x ^ (uint32_t)half, cur[r].y ^ (uint32_t)lane);
+            retire_stores();
+            wave_sync();
+            const uint32_t n32 = half ? (nb > 32u ? nb - 32u : 0u) : (nb < 32u ? nb : 32u);
+            store_stage(stage, wv, lane, recon + half * 32 * 256, n32 * 256u);
+        }
+    }
+}
+
+hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream, int num_cus) {
+    static const int per_cu = resident_per_cu(roundtrip_movement, kThreads);
+    const uint32_t nbatch = rt.ps.first[rt.ps.n];
+    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_rt
+    hipLaunchKernelGGL(roundtrip_movement, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt);
+    return hipGetLastError();
+}
+
 hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
                             hipStream_t stream, int num_cus) {
     const bool a = adaptive != 0, v = rt.ps.var[0] != nullptr, s = fallbacks != nullptr;

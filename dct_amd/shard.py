@@ -193,8 +193,10 @@ def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: 
     time the max over ranks:
       kernel-only : forward alone -> the aggregate rate of the GPUs' kernels;
       end-to-end  : forward + gather_coefficients -> what a caller that needs
-                    every coefficient on every rank gets (xGMI-bound).
-    Returns the two times, the blocks per step and the last gathered tensor."""
+                    every coefficient on every rank gets (xGMI-bound);
+      gather-only : gather_coefficients of the shard already computed -> the
+                    exchange alone, for its achieved bytes per second per rank.
+    Returns the three times, the blocks per step and the last gathered tensor."""
     import time
     import torch.distributed as dist
     total = sum(counts)
@@ -212,5 +214,25 @@ def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: 
 
     t_kernel, local = timed(lambda: forward(frames))
     t_e2e, full = timed(lambda: gather_coefficients(forward(frames), counts, group))
+    t_gather, _ = timed(lambda: gather_coefficients(local, counts, group))
     return {"blocks_per_step": total, "steps": steps, "kernel_s": t_kernel, "end_to_end_s": t_e2e,
-            "local": local, "full": full}
+            "gather_s": t_gather, "local": local, "full": full}
+
+
+# xGMI on an MI355X node is point-to-point, 7 links of ~153 GB/s per
+# GPU, one to each peer.  A rank of an N-rank gather can take in at most
+# (N - 1) x 153 GB/s (every peer pushing over its own link at once); a ring
+# that receives over one link per step is held to ~153 GB/s.
+XGMI_LINK_GBS = 153.0
+
+
+def xgmi_report(bytes_received: int, seconds_per_gather: float, world: int) -> dict:
+    """Achieved ingress of one rank's gather against the xGMI cost model, so a
+    scaling line says which regime its exchange ran in (direct pushes or a
+    ring) -- SURVEY 8(e), VERDICT r02 item 7."""
+    gbs = bytes_received / seconds_per_gather / 1e9 if seconds_per_gather > 0 else 0.0
+    direct = max(world - 1, 1) * XGMI_LINK_GBS
+    return {"bytes_received_per_rank": int(bytes_received), "us_per_gather": seconds_per_gather * 1e6,
+            "achieved_GBs_per_rank": gbs, "direct_estimate_GBs": direct, "frac_of_direct_estimate": gbs / direct,
+            "ring_one_link_estimate_GBs": XGMI_LINK_GBS, "frac_of_ring_estimate": gbs / XGMI_LINK_GBS,
+            "model": f"{max(world - 1, 1)} peer links x {XGMI_LINK_GBS:g} GB/s ingress (direct) vs one link (ring)"}

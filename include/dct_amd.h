@@ -35,14 +35,19 @@ extern "C" {
 
 /* Opaque per-configuration state: the host-computed tables (D of src/dct.c:17-30,
  * Q of src/quantization.c:51-99, fast-path scale and guard tables) uploaded to
- * the device that was current at creation, plus a small device workspace for
- * the exact tie path.  Calls on one plan must be ordered (one stream at a time,
- * or streams synchronised by the caller); use one plan per concurrent stream. */
+ * the device that was current at creation.  A plan is read-only after
+ * creation: one plan may serve several streams at once (the only mutable
+ * device state, the forward's tie stash, is kept per stream). */
 typedef struct dctq_plan dctq_plan;
 
 /* quality is clamped to 1..100 exactly as quant_init does (src/quantization.c:26-31).
- * A plan holds its tables and the forward kernel's tie stash in device memory
- * (about 256 MiB on a 256-CU MI355X); a plan is reusable and cheap to keep. */
+ * A plan holds only its ~4 KB of tables in device memory; it is reusable and
+ * cheap to keep (one per quality is fine).  The forward kernel's tie-path stash
+ * is the library's, one per (device, stream): allocated by the first forward
+ * launch on a stream that needs it (a launch with more 64-block batches than
+ * the device has resident waves), sized to that launch's grid (8 KiB per wave,
+ * at most 256 MiB on a 256-CU MI355X) and kept for later launches on the same
+ * stream.  Under hipGraph capture, run the launch once on the stream first. */
 int dctq_plan_create(int quality, int adaptive, dctq_plan **plan);
 /* Bind an existing reference-style context (block_size must be 8); its
  * quant_matrix VALUES are used, so a caller-modified table is honoured. */

@@ -279,6 +279,68 @@ def test_mid_size_tie_heavy_stream(T, dm):
                 assert int(cnt.item()) > 1000
 
 
+def test_plans_cheap_and_stash_per_stream(T, dm):
+    """VERDICT r02 item 6 / ADVICE r02: a plan holds only its tables; the forward's
+    tie stash is one per (device, stream), allocated lazily and sized to the
+    launched grid.  100 plans (q 1..100) cost < 1 GiB of device memory; a
+    multi-batch-per-wave forward of every tenth of them on ONE stream adds one
+    stash (<= 256 MiB); the same plan on two streams at once (each stream its
+    own stash) gives the oracle's coefficients on both."""
+    import oracle as O
+    px = dm.synth(4242, "uniform", 3840, 2160, 3)  # 388 800 blocks: > 16 waves x 256 CUs of batches -> v2 queue
+    outs = [T.empty((3 * 480 * 270, 64), dtype=T.int16, device="cuda") for _ in range(2)]
+    T.cuda.synchronize()
+    free0 = T.cuda.mem_get_info()[0]
+    plans = [dm.Plan(q, q % 2) for q in range(1, 101)]
+    T.cuda.synchronize()
+    free1 = T.cuda.mem_get_info()[0]
+    assert free0 - free1 < (1 << 30), (free0 - free1) / 2 ** 20
+    side = T.cuda.Stream()
+    for p in plans[::10]:
+        p.forward_quant(px, out=outs[0])
+    T.cuda.synchronize()
+    free2 = T.cuda.mem_get_info()[0]
+    assert free1 - free2 <= (256 << 20) + (16 << 20), (free1 - free2) / 2 ** 20
+    p = plans[50]  # q51, adaptive
+    side.wait_stream(T.cuda.current_stream())
+    p.forward_quant(px, out=outs[0])
+    with T.cuda.stream(side):
+        p.forward_quant(px, out=outs[1], stream=side)
+    T.cuda.synchronize()
+    host = px.cpu().numpy()
+    want = np.concatenate([O.forward_plane(host[f], 51, 1, 8) for f in range(3)])
+    assert np.array_equal(outs[0].cpu().numpy(), want)
+    assert np.array_equal(outs[1].cpu().numpy(), want)
+
+
+def test_bench_gpus2_gloo(T, dm):
+    """bench.py --gpus 2 with no launcher forms a 2-rank world by itself (its
+    children share this box's one GPU over gloo, as a rehearsal of the driver's
+    8-GPU run): the line says n_gpus 2 / world_size 2, the gather leg's own
+    slice survives the exchange, and the band split of one 4K 4:2:0 frame
+    gathers to the unsharded forward."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--steps", "2", "--warmup", "1",
+           "--no-cpu", "--frames", "2", "--total-frames", "4", "--gather-steps", "2", "--round-trip-steps", "1",
+           "--encode-steps", "1", "--ceiling-rounds", "0", "--prewarm-ms", "0"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["world_size"] == 2 and d["config"]["backend"] == "gloo", d["config"]
+    g, b = d["gather"], d["band"]
+    assert g["world_size"] == 2 and g["own_slice_intact"] is True, g
+    assert b["gathered_equals_unsharded"] is True, b
+    assert g["xgmi"]["bytes_received_per_rank"] == g["bytes_received_per_rank"] > 0, g
+    assert b["xgmi"]["achieved_GBs_per_rank"] > 0, b
+
+
 def test_dist_legs_rccl_one_rank(T, dm):
     """The N>1 legs of bench.py over a real RCCL process group: one rank on this GPU
     (bench.py --dist-legs).  The gather leg (BASELINE configs[3]: all_gather_into_tensor
@@ -334,6 +396,10 @@ def test_bench_json_contract(T, dm):
         assert k in cb, k
     assert cb["kind"] == "reference" and cb["value"] > 0 and cb["cores"] >= 1
     assert d["parity_check"] is True and d["encode"]["huffman"]["parity_check_chroma0"] is True
+    rt = d["round_trip"]
+    assert rt["parity_check"] is True, rt.get("parity")
+    mc = rt["movement_ceiling"]
+    assert 0 < mc["fused_frac"] < 1 and 0 < mc["movement_frac"] < 1 and 0 < mc["flat_124_frac"] < 1, mc
 
 
 def test_diag_stream_moves_bytes(T, dm):
@@ -504,6 +570,48 @@ def test_round_trip_planes_fused(T, dm):
                 # and the same floats as the unfused dctq_inverse
                 ri = plan.inverse(c, var_num=v).cpu().numpy()
                 assert np.abs(ri - r.cpu().numpy()).max() <= 2e-5
+
+
+@pytest.mark.parametrize("ad", [0, 1])
+def test_round_trip_full_size_4k420(T, dm, ad):
+    """BASELINE configs[4] at full size: round_trip_planes over 16 4K 4:2:0 frames
+    (bench.py's seeds and multi-plane launch: 3.1 M blocks, so the x8 grid gives
+    its waves more than one batch each), every block checked -- coefficients
+    bit-exact against the oracle's forward_plane, recon within 1e-4 of its
+    dct_inverse(dequantize()) + 128 -- and luma frame 0's PSNR equal to the
+    oracle pipeline's with the reference formula (tests/test_entropy.c:368-393;
+    src/quantization.c:133-151, src/dct.c:80-105)."""
+    import math
+    import oracle as O
+    F, q = 16, 50
+    luma = dm.synth(12345, "uniform", 3840, 2160, F)
+    chroma = dm.synth(12345 + 50000, "uniform", 1920, 1080, 2 * F)
+    (cy, cc), (ry, rc) = dm.Plan(q, ad).round_trip_planes([luma, chroma])
+    assert (luma.shape[0] * 480 * 270 + chroma.shape[0] * 240 * 135) // 64 > 8 * 4 * 4 * 256  # > 1 batch per wave
+    threads = min(16, os.cpu_count() or 1)
+    psnr_gpu = psnr_ref = None
+    for px, coef, rec, per in ((luma, cy, ry, 480 * 270), (chroma, cc, rc, 240 * 135)):
+        host_px = px.cpu().numpy()
+        for f in range(px.shape[0]):
+            got_c = coef[f * per:(f + 1) * per].cpu().numpy()
+            got_r = rec[f * per:(f + 1) * per].cpu().numpy().astype(np.float64)
+            want_c = O.forward_plane(host_px[f], q, ad, threads)
+            assert np.array_equal(got_c, want_c), (ad, tuple(px.shape), f, int((got_c != want_c).sum()))
+            want_r = O.inverse_plane(want_c, q, ad, O.plane_variance(host_px[f]) if ad else None) + 128.0
+            err = float(np.abs(got_r - want_r).max())
+            assert err <= 1e-4, (ad, tuple(px.shape), f, err)
+            if px is luma and f == 0:
+                h, w = host_px.shape[1:]
+                blocks = host_px[0].reshape(h // 8, 8, w // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
+                blocks = blocks.astype(np.float64)
+
+                def psnr(r):
+                    mse = float(((blocks - np.clip(r, 0, 255)) ** 2).mean())
+                    return 10.0 * math.log10(255.0 * 255.0 / mse)
+                psnr_gpu, psnr_ref = psnr(got_r), psnr(want_r)
+    assert abs(psnr_gpu - psnr_ref) <= 1e-3, (psnr_gpu, psnr_ref)
+    # SURVEY 6: the bug-compatible 1/Q dequantization gives ~11 dB on noise, adaptive ~23 dB
+    assert (psnr_ref < 15.0) if ad == 0 else (psnr_ref > 15.0), psnr_ref
 
 
 def test_round_trip_exact_count_matches_forward(T, dm):

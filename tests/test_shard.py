@@ -89,7 +89,11 @@ def _worker(rank, world, port, q):
 
         r = shard.strong_gather_leg(forward, stack[lo:hi], counts, 2, torch.device("cpu"))
         assert r["blocks_per_step"] == total * per and r["steps"] == 2
-        assert r["kernel_s"] > 0 and r["end_to_end_s"] > 0
+        assert r["kernel_s"] > 0 and r["end_to_end_s"] > 0 and r["gather_s"] > 0
+        x = shard.xgmi_report((total * per - counts[rank]) * 128, r["gather_s"] / r["steps"], world)
+        assert x["bytes_received_per_rank"] == (total * per - counts[rank]) * 128
+        assert x["direct_estimate_GBs"] == (world - 1) * shard.XGMI_LINK_GBS
+        assert abs(x["frac_of_direct_estimate"] * x["direct_estimate_GBs"] - x["achieved_GBs_per_rank"]) < 1e-9
         want = np.concatenate([O.forward_plane(f.numpy(), 75, 0) for f in stack])
         assert np.array_equal(r["full"].numpy(), want), "strong-scaling gather differs"
         assert np.array_equal(r["local"].numpy(), want[sum(counts[:rank]):sum(counts[:rank + 1])])
