@@ -265,6 +265,9 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
     if (STATS && lane == 0) atomicAdd(fallbacks, (unsigned long long)take);
 }
 
+#ifndef DCTQ_LAST_INPLACE
+#define DCTQ_LAST_INPLACE 1  // a wave's last batch empties the queue before its stores and resolves in place
+#endif
 #ifndef DCTQ_INSTAGE_LANES
 // A batch with at least this many flagged blocks resolves its ties in the stage,
 // before its stores (resolve_in_stage); sparser batches queue them.  65 = never.
@@ -310,14 +313,20 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     // A full round of entries from earlier batches drains HERE, before this
     // batch's stores are issued: vmcnt counts in issue order, so a drain after
     // them would wait for all 8 KiB of them before its first stash load returns.
-    if (qn >= 64) {
+    // The wave's LAST batch (DCTQ_LAST_INPLACE) drains every entry still queued
+    // here -- behind the previous batch's long-issued stores, not behind its own
+    // -- and resolves its own ties in the stage, so the wave ends with its last
+    // stores: no final drain (vmcnt(0) behind 8 KiB of fresh stores, stash
+    // loads, fp64, patches) in the kernel's tail.
+    const bool last = DCTQ_LAST_INPLACE && g + step >= ps.first[ps.n];
+    while (qn >= 64 || (last && qn > 0)) {
         if (DCTQ_ABLATE & 16) qn = 0;
         else drain_queue<ADAPTIVE, STATS>(ps, dev, qb, qc, ring, qn, lane, fallbacks);
     }
 
     if (!valid || (DCTQ_ABLATE & 8)) mlo = mhi = 0;
-    if (DCTQ_INSTAGE_LANES <= 64 &&
-        __builtin_popcountll(__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) >= DCTQ_INSTAGE_LANES)
+    const int nflag = __builtin_popcountll(__builtin_amdgcn_ballot_w64((mlo | mhi) != 0));
+    if ((DCTQ_INSTAGE_LANES <= 64 && nflag >= DCTQ_INSTAGE_LANES) || (last && nflag > 0))
     {
         // tie-heavy batch: resolved in the stage before its stores (no stash, no patches)
         const uint32_t n = resolve_ties_compact<ADAPTIVE>(tab, cur, stage, qc + qn, lane, wv, mlo, mhi);

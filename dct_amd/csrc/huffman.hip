@@ -38,6 +38,8 @@
 // noise, most natural content) skip the sort: narrow_counts below.  VALU-bound
 // (DESIGN.md 3.8).
 // DCTQ_HUF_MIN_WAVES (launch bound, default 3 waves/SIMD: 168 VGPRs) is an A/B knob.
+#include <type_traits>
+
 #include "dctq_internal.h"
 #include "fdct8_core.h"
 
@@ -440,23 +442,34 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
     {
         uint32_t d[32];
         tile_row<FWD>(mine, lane, d);
-        {
-            // nonzeros: unsigned min(h, 1) is 1 for any nonzero half; two packed 16-bit partial sums
+        last_zero = (d[31] >> 16) == 0u;
+        // Nonzeros of dwords [k0, k1): unsigned min(h, 1) is 1 for any nonzero half;
+        // the packed 0/1 pairs summed three at a time as plain dwords (each half
+        // stays below 2^16), then the two halves added.
+        auto nonzeros = [&](auto k0c, auto k1c) {
+            constexpr int k0 = decltype(k0c)::value, k1 = decltype(k1c)::value;
             typedef unsigned short u2 __attribute__((ext_vector_type(2)));
             const u2 one = {1, 1};
-            u2 acc = {0, 0};
             const uint32_t one32 = __builtin_bit_cast(uint32_t, one);
+            uint32_t m[k1 - k0];
 #pragma unroll
-            for (int k = 0; k < 32; ++k) {
-                uint32_t m;  // inline asm: LLVM turns the packed min into compares and selects
-                asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(d[k]), "v"(one32));
-                acc += __builtin_bit_cast(u2, m);
+            for (int k = k0; k < k1; ++k)  // inline asm: LLVM turns the packed min into compares and selects
+                asm("v_pk_min_u16 %0, %1, %2" : "=v"(m[k - k0]) : "v"(d[k]), "v"(one32));
+            uint32_t acc0 = 0, acc1 = 0;  // two chains: no dependent back-to-back adds
+#pragma unroll
+            for (int k = 0; k + 1 < k1 - k0; k += 4) {
+                acc0 = m[k] + m[k + 1] + acc0;
+                if (k + 3 < k1 - k0) acc1 = m[k + 2] + m[k + 3] + acc1;
             }
-            nz = (uint32_t)acc.x + (uint32_t)acc.y;
-        }
-        last_zero = (d[31] >> 16) == 0u;
-        if (__builtin_amdgcn_ballot_w64(nz > 32)) {
-            // dense tile: the span of its values, zeros included (packed 16-bit min/max)
+            const uint32_t acc = acc0 + acc1;
+            return (acc & 0xFFFFu) + (acc >> 16);
+        };
+        // The span test (packed 16-bit min/max) runs first on tiles that look dense:
+        // rows 0-1 (dwords 0..7) with more than 7 nonzeros in some lane.  A dense
+        // tile of narrow span takes the narrow path, which counts its own symbols,
+        // so its exact nonzero count is never needed; the estimate only picks a
+        // path (every path gives the same sizes).
+        auto span_test = [&] {
             typedef short s2 __attribute__((ext_vector_type(2)));
             s2 mn = __builtin_bit_cast(s2, d[0]), mx = mn;
 #pragma unroll
@@ -469,6 +482,13 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
             const int32_t vmax = mx.x > mx.y ? mx.x : mx.y;
             span = (uint32_t)(vmax - vmin + 1);
             narrow = !__builtin_amdgcn_ballot_w64(lane < nb && vmax - vmin >= 64);
+        };
+        const bool looks_dense =
+            __builtin_amdgcn_ballot_w64(nonzeros(std::integral_constant<int, 0>{}, std::integral_constant<int, 8>{}) > 7u) != 0;
+        if (looks_dense) span_test();
+        if (!narrow) {
+            nz = nonzeros(std::integral_constant<int, 0>{}, std::integral_constant<int, 32>{});
+            if (!looks_dense && __builtin_amdgcn_ballot_w64(nz > 32)) span_test();  // dense after all
         }
     }
     // the paths re-read the row: a memory clobber keeps the compiler from reusing
