@@ -745,6 +745,18 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
                             for k in cases}}
 
 
+def build_record():
+    """Which library this line measured: the sha256 of the loaded libdct_amd.so
+    and whether it is the one dct_amd/build.py's manifest (build_info.json:
+    sha256 of every source it was built from) says it built."""
+    import hashlib
+    from dct_amd import build as B
+    sha = hashlib.sha256(open(dct_amd.LIB_PATH, "rb").read()).hexdigest()
+    info = B.build_info()
+    return {"lib_sha256": sha, "manifest_lib_sha256_matches": info.get("lib_sha256") == sha,
+            "built_utc": info.get("built_utc"), "hipcc": info.get("hipcc")}
+
+
 def traffic_for(args, launches):
     """PMC HBM traffic of this exact configuration, or None with the reason: the
     stored measurement (tools/pmc_traffic.py) must match frames, kind, quality,
@@ -940,6 +952,7 @@ def main():
             "encode": encode,
             "small_frame": small,
             "gpu": gpu_identity(),
+            "build": build_record(),
             "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
                     "reference-order recomputation for guard-band (tie) coefficients",
         }

@@ -32,13 +32,45 @@ HEADERS = ["dctq_internal.h", "plan.h", "dctq_diag.h", "fdct8_bound.h", "host_ta
 ARCH = "gfx950"
 
 
+INFO = os.path.join(HERE, "build_info.json")
+
+
+def _sha256(path: str) -> str:
+    import hashlib
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _inputs() -> dict:
+    """Every file the libraries are built from (sources, headers, public headers, this script) -> sha256."""
+    deps = [os.path.join(CSRC, f) for f in SOURCES + DIAG_SOURCES + HEADERS] + [os.path.abspath(__file__)]
+    deps += [os.path.join(ROOT, "include", f) for f in sorted(os.listdir(os.path.join(ROOT, "include")))]
+    return {os.path.relpath(d, ROOT): _sha256(d) for d in deps}
+
+
+def build_info() -> dict:
+    """The manifest the last build wrote (dct_amd/build_info.json), or {}."""
+    import json
+    try:
+        with open(INFO) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
 def _stale() -> bool:
+    """Content-gated: rebuild unless both libraries exist and the manifest of the
+    last build names exactly these inputs and these library bytes."""
     if not os.path.exists(LIB) or not os.path.exists(DIAG_LIB):
         return True
-    t = min(os.path.getmtime(LIB), os.path.getmtime(DIAG_LIB))
-    deps = [os.path.join(CSRC, f) for f in SOURCES + DIAG_SOURCES + HEADERS] + [__file__]
-    deps += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
-    return any(os.path.getmtime(d) > t for d in deps)
+    info = build_info()
+    return (info.get("inputs") != _inputs() or info.get("lib_sha256") != _sha256(LIB)
+            or info.get("diag_sha256") != _sha256(DIAG_LIB) or info.get("flags") != _portable_flags())
+
+
+def _portable_flags() -> list:
+    """_flags() with the checkout's path replaced, so a manifest stays valid in a copy of the tree."""
+    return [f.replace(ROOT, "$ROOT") for f in _flags()]
 
 
 def _flags():
@@ -102,6 +134,14 @@ def build(force: bool = False, verbose: bool = False) -> str:
         if out.returncode != 0:
             raise RuntimeError("hipcc link failed:\n" + out.stdout + out.stderr)
         os.replace(lib + ".tmp", lib)
+    import json
+    import time
+    ver = subprocess.run(["hipcc", "--version"], capture_output=True, text=True).stdout.strip().splitlines()
+    info = {"lib_sha256": _sha256(LIB), "diag_sha256": _sha256(DIAG_LIB), "inputs": _inputs(), "flags": _portable_flags(),
+            "hipcc": ver[:2], "arch": ARCH, "built_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
+    with open(INFO + ".tmp", "w") as f:
+        json.dump(info, f, indent=1, sort_keys=True)
+    os.replace(INFO + ".tmp", INFO)
     return LIB
 
 

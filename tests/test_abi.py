@@ -154,3 +154,19 @@ def test_constant_block_dc_table(lib):
             want = O.quantize(O.forward(x), q, 0, 0.0)[0, 0]
             assert tab[v] == want, (q, v, tab[v], want)
             assert O.quantize(O.forward(x), q, 1, O.variance(x))[0, 0] == want  # adaptive keeps Q for the DC
+
+
+def test_build_manifest_matches_library():
+    """build() is content-gated: dct_amd/build_info.json records the sha256 of every
+    source, header and flag the libraries were built from and of the two libraries;
+    the shipped libdct_amd.so is the one it describes (bench.py reports the same
+    hash in its `build` record)."""
+    import hashlib
+
+    from dct_amd import build as B
+    info = B.build_info()
+    assert info, "dct_amd/build_info.json missing: run python -m dct_amd.build"
+    assert info["lib_sha256"] == hashlib.sha256(open(B.LIB, "rb").read()).hexdigest()
+    assert info["diag_sha256"] == hashlib.sha256(open(B.DIAG_LIB, "rb").read()).hexdigest()
+    assert info["inputs"] == B._inputs(), "sources changed since the last build"
+    assert not B._stale()
