@@ -114,12 +114,25 @@ def spawn_ranks(n: int) -> int:
     sk.bind(("127.0.0.1", 0))
     port = sk.getsockname()[1]
     sk.close()
+    def die_with_parent():  # in the child, before it runs anything: SIGTERM if this launcher dies
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else sys.stderr))
+                                      stdout=None if r == 0 else sys.stderr, preexec_fn=die_with_parent))
+
+    def forward(signum, _frame):  # a time limit on this launcher reaches the ranks too
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
     rc = 0
     live = list(procs)
     while live:
