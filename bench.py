@@ -179,10 +179,24 @@ def gpu_identity():
     boxes of this pool differ by up to ~15 % on the same bytes, and the
     bench's own ceilings are the normaliser; this says which box a line came from."""
     import re
+    import shutil
     import subprocess
+    if "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        # under rocprofv3 every child process gets the profiler preloaded (with --pmc it
+        # initialises the GPU), and rocm-smi's `#!/usr/bin/env python3` would then exec
+        # after GPU initialisation: skip the query in profiling runs
+        return None
+    smi = shutil.which("rocm-smi") or "/opt/rocm/bin/rocm-smi"
     try:
-        r = subprocess.run(["rocm-smi", "--showserial", "--showmemvendor", "--showmemorypartition",
-                            "--showcomputepartition"], capture_output=True, text=True, timeout=30)
+        with open(smi, "rb") as f:
+            first = f.readline()
+    except OSError:
+        return None
+    script = first.startswith(b"#!") and b"python" in first  # run it with this interpreter: no env hop
+    cmd = ([sys.executable, smi] if script else [smi]) + ["--showserial", "--showmemvendor",
+                                                         "--showmemorypartition", "--showcomputepartition"]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=30)
     except (OSError, subprocess.SubprocessError):
         return None
     keys = {"Serial Number": "serial", "GPU memory vendor": "hbm_vendor", "Memory Partition": "memory_partition",
