@@ -96,6 +96,7 @@ __device__ __forceinline__ void sort_net(uint32_t (&a)[N]) {
 // absorbs "no leaf" adds, so the count loops stay branch-free.  65 buckets =
 // 8 320 B, inside the wave's 9 KiB tile stage.
 constexpr int kHistBytes = 65 * 128;
+static_assert(kHistBytes <= kHufWaveLds, "the histogram fits the wave's tile stage");
 __device__ __forceinline__ void hist_add(char *h, int w, int lane, uint32_t n) {
     __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(h + w * 128 + (lane & ~1) * 2), n << (16 * (lane & 1)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -270,12 +271,27 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
 //  3. readout: each counter is read AND cleared by one ds_and_rtn (the wave's
 //     byte only), and adds one leaf at its frequency to the weight histogram
 //     (row 0 absorbs empty counters);
-//  4. merge as in the dense path (each lane jumps to its next occupied bucket),
-//     every bucket read AND cleared as it is processed.
-// Returns the symbol count and the WPL.
+//  4. the weight rows are read back (and cleared) and merged in registers.
+// narrow_leaves runs steps 1-3 and ISSUES the read-back of step 4 (its results
+// stay in flight in NarrowLeaves until narrow_merge extracts the wave's bytes
+// and runs the register merge).  A software-pipelined kernel loop that merged one
+// tile while the next tile's LDS phases were in flight measured no faster
+// (profiles/r03/huffman_restructure_ab.log).
+#ifndef DCTQ_HUF_HEAVY_ROWS
+#define DCTQ_HUF_HEAVY_ROWS 4
+#endif
+constexpr int kHeavyRows = DCTQ_HUF_HEAVY_ROWS;  // weight rows 17.. read back without waiting (q50 noise: largest leaf ~20)
+struct NarrowLeaves {
+    uint32_t light[16];  // weight rows 1..16 as read (the wave's byte at 8 * wave)
+    uint32_t heavy[kHeavyRows];  // weight rows 17..16 + kHeavyRows as read, when hrows > 16
+    uint32_t hn, hs, hmn, hmx;  // leaves of the rows past those (read at once: rare): count, sum, min, max
+    uint32_t count;      // symbols of the block
+    uint32_t hrows;      // wave-uniform: 16 + kHeavyRows when heavy[] was read, else 16
+};
+
 template <bool FWD = false, typename NextTile>
-__device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lane, int wv, int32_t vmin, uint32_t span,
-                                            bool last_zero, uint32_t &count, uint32_t &wpl, NextTile next_tile) {
+__device__ __forceinline__ void narrow_leaves(const char *mine, char *ctr, int lane, int wv, int32_t vmin,
+                                              uint32_t span, bool last_zero, NextTile next_tile, NarrowLeaves &L) {
     uint32_t d[32];
     tile_row<FWD>(mine, lane, d);
     // the row is in registers and the stage is free: the next tile streams in meanwhile
@@ -286,6 +302,9 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
     const uint32_t sh = 8u * (uint32_t)wv, inc = 1u << sh, keep = ~(0xFFu << sh);  // the wave's byte of it
     const u16x2 off = {(unsigned short)(-vmin), (unsigned short)(-vmin)};
     auto at = [&](uint32_t row) { return reinterpret_cast<uint32_t *>(ctr + (row << 8) + base); };
+    auto take_raw = [&](uint32_t row) {  // row's dword, the wave's byte cleared in LDS
+        return __hip_atomic_fetch_and(at(row), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    };
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         const uint32_t sl = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, d[k]) + off);  // slots, < 64 each
@@ -298,86 +317,130 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
     uint32_t zeros = 0;
     if (vmin <= 0 && vmin > -64) {
         const uint32_t z = (uint32_t)(-vmin);
-        zeros = (__hip_atomic_fetch_and(at(z), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+        zeros = (take_raw(z) >> sh) & 0xFFu;
         if (last_zero) __hip_atomic_fetch_add(at(z), inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
-    count = 64u - zeros + (last_zero ? 1u : 0u);
+    L.count = 64u - zeros + (last_zero ? 1u : 0u);
     // readout: every counter read and cleared, THEN the leaves added (the weight
     // histogram reuses the rows).  Only rows below the wave's largest span hold
-    // counts (q50 noise: 32 of 64), in wave-uniform chunks of 8 rows.  A counter
-    // is kept as its leaf's address: one v_perm moves the wave's byte of the
-    // returned dword into byte 1 (the row) over the lane's byte 0 -- no extract --
-    // and the largest address gives the largest leaf weight.
-    const uint32_t leaf_sel = 0x0C0C0000u | ((4u + (uint32_t)wv) << 8);
-    uint32_t a[64];
+    // counts (q50 noise: 32-40 of 64): the first nck wave-uniform chunks of 8 rows
+    // (span conditions are monotone in the chunk).  Rows of skipped chunks are
+    // never read, so nothing is materialised for them.
+    int nck = 1;
+#pragma unroll
+    for (int c8 = 1; c8 < 8; ++c8) nck += __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8)) != 0 ? 1 : 0;
+    uint32_t raw[64];
 #pragma unroll
     for (int c8 = 0; c8 < 8; ++c8) {
-        if (c8 == 0 || __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8))) {
+        if (c8 < nck) {
 #pragma unroll
-            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_)
-                a[s_] = __builtin_amdgcn_perm(
-                    __hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT), base, leaf_sel);
-        } else {
-#pragma unroll
-            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) a[s_] = base;
+            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) raw[s_] = take_raw((uint32_t)s_);
         }
     }
 #if DCTQ_HUF_ABLATE == 1  // timing: count + readout only
-    wpl = a[0] + a[63];
+    L.light[0] = raw[0] + raw[7];
+    L.hrows = 16;
+    L.hn = L.hs = L.hmx = 0;
+    L.hmn = 0xFFu;
     return;
 #endif
+    // A counter is kept as its leaf's address: one v_perm moves the wave's byte of
+    // the returned dword into byte 1 (the row) over the lane's byte 0 -- no extract
+    // -- and the largest address gives the largest leaf weight.
+    const uint32_t leaf_sel = 0x0C0C0000u | ((4u + (uint32_t)wv) << 8);
     uint32_t amax = base;
 #pragma unroll
     for (int c8 = 0; c8 < 8; ++c8) {
-        if (c8 == 0 || __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8))) {
+        if (c8 < nck) {
 #pragma unroll
             for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) {
-                amax = a[s_] > amax ? a[s_] : amax;
-                __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(ctr + a[s_]), inc, __ATOMIC_RELAXED,
+                const uint32_t a = __builtin_amdgcn_perm(raw[s_], base, leaf_sel);
+                amax = a > amax ? a : amax;
+                __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(ctr + a), inc, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WAVEFRONT);
             }
         }
     }
     const uint32_t lmax = amax >> 8;  // the largest leaf weight
-#if DCTQ_HUF_ABLATE == 2  // timing: leaf adds, then a plain clear instead of the merge
+    (void)take_raw(0);  // row 0: the empties
+#if DCTQ_HUF_ABLATE == 2  // timing: leaf adds, then a plain clear instead of the read-back
+    uint32_t acc = 0;
 #pragma unroll
-    for (int s_ = 0; s_ < 65; ++s_) wpl += (__hip_atomic_fetch_and(at(s_), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+    for (int s_ = 1; s_ < 65; ++s_) acc += take_raw((uint32_t)s_);
+    L.light[0] = acc;
+    L.hrows = 16;
+    L.hn = L.hs = L.hmx = 0;
+    L.hmn = 0xFFu;
     return;
 #endif
-    // ---- merge in registers (no LDS round trip inside the merge; Python model:
-    // tests/test_oracle.py::register_merge_wpl).  Leaf weights <= 16 are read back
-    // from their rows (each row read AND cleared) and scanned w = 1..16 as the
-    // bucket merge.  A pending merge makes ONE node of weight p + w in (w, 2w), and
-    // successive ones are strictly heavier, so they are bits of a mask.  Nodes
-    // heavier than 16 (leaves, pairs of w >= 9, pending merges) are at most 3,
-    // because all node weights add up to the symbol count (<= 65): their count,
-    // sum, min and max give them sorted, and with the pending node (the lightest)
-    // they finish in closed form.
-    (void)__hip_atomic_fetch_and(at(0), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);  // row 0: the empties
-    auto take = [&](uint32_t w) {  // row w's count, cleared
-        return (__hip_atomic_fetch_and(at(w), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
-    };
+    // weight rows 1..16 issued together (independent reads, all in flight; their
+    // results are used by narrow_merge), each row cleared
+#pragma unroll
+    for (int w = 1; w <= 16; ++w) L.light[w - 1] = take_raw((uint32_t)w);
+    // rows 17..16 + kHeavyRows read unconditionally when the wave has a leaf there
+    // (rows past a lane's largest leaf read as zero): no branch per row, so the
+    // results stay in flight in registers
+    L.hrows = __builtin_amdgcn_ballot_w64(lmax > 16) ? 16u + kHeavyRows : 16u;
+    if (L.hrows > 16) {
+#pragma unroll
+        for (int r = 17; r <= 16 + kHeavyRows; ++r) L.heavy[r - 17] = take_raw((uint32_t)r);
+    }
+    // rows past those (a leaf of that many copies of one value): read one by one
+    L.hn = 0;
+    L.hs = 0;
+    L.hmn = 0xFFu;
+    L.hmx = 0;
+    for (uint32_t r = 17 + kHeavyRows; __builtin_amdgcn_ballot_w64(r <= lmax); ++r) {
+        const uint32_t k = (take_raw(r) >> sh) & 0xFFu;
+        L.hn += k;
+        L.hs += k * r;
+        L.hmn = (k && L.hmn == 0xFFu) ? r : L.hmn;
+        L.hmx = k ? r : L.hmx;
+    }
+}
+
+// ---- merge in registers (no LDS round trip inside the merge; Python model:
+// tests/test_oracle.py::register_merge_wpl).  Leaf weights <= 16 (their rows
+// read back by narrow_leaves) are scanned w = 1..16 as the bucket merge.  A
+// pending merge makes ONE node of weight p + w in (w, 2w), and successive ones
+// are strictly heavier, so they are bits of a mask.  Nodes heavier than 16
+// (leaves, pairs of w >= 9, pending merges) are at most 3, because all node
+// weights add up to the symbol count (<= 65): their count, sum, min and max give
+// them sorted, and with the pending node (the lightest) they finish in closed form.
+// Returns the WPL.
+__device__ __forceinline__ uint32_t narrow_merge(const NarrowLeaves &L, int wv) {
+    const uint32_t sh = 8u * (uint32_t)wv;
+#if DCTQ_HUF_ABLATE == 1 || DCTQ_HUF_ABLATE == 2
+    return L.light[0] >> sh;
+#endif
     uint32_t cnt[17];
 #pragma unroll
-    for (int w = 1; w <= 16; ++w) cnt[w] = take((uint32_t)w);  // independent reads, all in flight
-    // heavy nodes: count, sum, min, max
+    for (int w = 1; w <= 16; ++w) cnt[w] = (L.light[w - 1] >> sh) & 0xFFu;
+    // heavy leaves: rows 17..16 + kHeavyRows, then the rarer rows past them (all heavier)
     uint32_t hn = 0, hs = 0, hmn = 0xFFu, hmx = 0;
-    for (uint32_t r = 17; __builtin_amdgcn_ballot_w64(r <= lmax); ++r) {  // heavy leaves, rows ascending
-        const uint32_t k = take(r);
-        hn += k;
-        hs += k * r;
-        hmn = (k && hmn == 0xFFu) ? r : hmn;
-        hmx = k ? r : hmx;
-    }
-#if DCTQ_HUF_ABLATE == 3  // timing: leaf adds and read-back, no merge
-    wpl = hn + hs;
 #pragma unroll
-    for (int w = 1; w <= 16; ++w) wpl += cnt[w];
-    return;
+    for (int r = 17; r <= 16 + kHeavyRows; ++r) {
+        if (L.hrows > 16) {
+            const uint32_t k = (L.heavy[r - 17] >> sh) & 0xFFu;
+            hn += k;
+            hs += k * (uint32_t)r;
+            hmn = (k && hmn == 0xFFu) ? (uint32_t)r : hmn;
+            hmx = k ? (uint32_t)r : hmx;
+        }
+    }
+    hn += L.hn;
+    hs += L.hs;
+    hmn = min(hmn, L.hmn);
+    hmx = max(hmx, L.hmx);
+#if DCTQ_HUF_ABLATE == 3  // timing: leaves and read-back, no merge
+    uint32_t s3 = hn + hs;
+#pragma unroll
+    for (int w = 1; w <= 16; ++w) s3 += cnt[w];
+    return s3;
 #endif
     uint32_t p = 0, pm = 0;  // the pending node's weight (0: none); pending-merge nodes (bit = weight)
     uint32_t qn = 0, qs = 0, qmn = 0xFFu, qmx = 0;  // heavy pairs (weights 2w, w = 9..16, ascending)
-    wpl = 0;
+    uint32_t wpl = 0;
 #pragma unroll
     for (uint32_t w = 1; w <= 16; ++w) {
         uint32_t c = cnt[w];
@@ -420,7 +483,7 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
     } else {
         fin = hn == 3 ? 2 * (h1 + h2) + h3 : hn == 2 ? h1 + h3 : 0u;
     }
-    wpl += fin;
+    return wpl + fin;
 }
 
 #ifndef DCTQ_HUF_BITS_AUX
@@ -428,21 +491,26 @@ __device__ __forceinline__ void narrow_tile(const char *mine, char *ctr, int lan
 // passes on one box (profiles/r02/huffman_dma_ab.log).
 #define DCTQ_HUF_BITS_AUX 2
 #endif
-// One tile in the wave's stage (Huffman layout, blocks past the end zeroed): the
-// bit count of every lane's block.  next_tile() is called once the stage may be
-// overwritten (the next tile's DMA, or nothing).
-template <bool FWD = false, typename NextTile>
-__device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, int wv, int nb, NextTile next_tile) {
-    bool dma_issued = false;
-    uint32_t nz = 0;
+// A tile's classification (tile_row layout, blocks past the end zeroed).
+struct TileClass {
+    uint32_t nz;        // the lane's nonzero count (exact unless narrow: then 0, unused)
     bool last_zero;     // c[63] == 0: value 0 is a symbol once
-    bool narrow = false;  // a dense tile whose every block has its values (zeros included) within 64 integers
-    int32_t vmin = 0;
-    uint32_t span = 64;  // the lane's values (zeros included) lie in [vmin, vmin + span)
+    bool narrow;        // wave-uniform: a dense tile whose every block has its values (zeros included) within 64 integers
+    int32_t vmin;
+    uint32_t span;      // the lane's values (zeros included) lie in [vmin, vmin + span)
+};
+
+template <bool FWD = false>
+__device__ __forceinline__ TileClass classify(const char *mine, int lane, int nb) {
+    TileClass c;
+    c.nz = 0;
+    c.narrow = false;
+    c.vmin = 0;
+    c.span = 64;
     {
         uint32_t d[32];
         tile_row<FWD>(mine, lane, d);
-        last_zero = (d[31] >> 16) == 0u;
+        c.last_zero = (d[31] >> 16) == 0u;
         // Nonzeros of dwords [k0, k1): unsigned min(h, 1) is 1 for any nonzero half;
         // the packed 0/1 pairs summed three at a time as plain dwords (each half
         // stays below 2^16), then the two halves added.
@@ -478,23 +546,33 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
                 mn = __builtin_elementwise_min(mn, x);
                 mx = __builtin_elementwise_max(mx, x);
             }
-            vmin = mn.x < mn.y ? mn.x : mn.y;
+            c.vmin = mn.x < mn.y ? mn.x : mn.y;
             const int32_t vmax = mx.x > mx.y ? mx.x : mx.y;
-            span = (uint32_t)(vmax - vmin + 1);
-            narrow = !__builtin_amdgcn_ballot_w64(lane < nb && vmax - vmin >= 64);
+            c.span = (uint32_t)(vmax - c.vmin + 1);
+            c.narrow = !__builtin_amdgcn_ballot_w64(lane < nb && vmax - c.vmin >= 64);
         };
         const bool looks_dense =
             __builtin_amdgcn_ballot_w64(nonzeros(std::integral_constant<int, 0>{}, std::integral_constant<int, 8>{}) > 7u) != 0;
         if (looks_dense) span_test();
-        if (!narrow) {
-            nz = nonzeros(std::integral_constant<int, 0>{}, std::integral_constant<int, 32>{});
-            if (!looks_dense && __builtin_amdgcn_ballot_w64(nz > 32)) span_test();  // dense after all
+        if (!c.narrow) {
+            c.nz = nonzeros(std::integral_constant<int, 0>{}, std::integral_constant<int, 32>{});
+            if (!looks_dense && __builtin_amdgcn_ballot_w64(c.nz > 32)) span_test();  // dense after all
         }
     }
     // the paths re-read the row: a memory clobber keeps the compiler from reusing
     // (and holding) these 32 registers across the choice
     asm volatile("" ::: "memory");
-    // ---- runs of equal values -> histogram of frequencies (the tile's LDS is reused)
+    return c;
+}
+
+// The sparse and dense paths of a tile that is not narrow: runs of equal values
+// -> histogram of frequencies in the wave's stage, then the bucket merge; calls
+// next_tile() once the stage is free.  Returns the bit counts.
+template <bool FWD = false, typename NextTile>
+__device__ __forceinline__ uint32_t sort_tile_bits(char *mine, int lane, int nb, const TileClass &cl,
+                                                   NextTile next_tile) {
+    const uint32_t nz = cl.nz;
+    const bool last_zero = cl.last_zero;
     uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
     uint32_t nodes = last_zero ? 1u : 0u;
     uint32_t lmax = last_zero ? 1u : 0u;  // the largest leaf weight (dense paths)
@@ -505,21 +583,13 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
     const bool lane_merge = dense;  // the dense paths merge per lane (occupancy mask)
 #endif
     uint32_t wpl = 0, pending = 0;
-#ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
-    if (true) {
-    } else
-#endif
-    if (narrow) {
-        dma_issued = true;
-        narrow_tile<FWD>(mine, ctr, lane, wv, vmin, span, last_zero, count, wpl, next_tile);  // the zero leaf included
-    } else {
-        if (!__builtin_amdgcn_ballot_w64(nz > 16))
-            sparse_runs<16, FWD>(mine, lane, nodes, lmax);
-        else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-            sparse_runs<32, FWD>(mine, lane, nodes, lmax);
-        else
-            dense_runs<FWD>(mine, lane, nodes, lmax);
-        if (last_zero) hist_add(mine, 1, lane, 1);
+    if (!__builtin_amdgcn_ballot_w64(nz > 16))
+        sparse_runs<16, FWD>(mine, lane, nodes, lmax);
+    else if (!__builtin_amdgcn_ballot_w64(nz > 32))
+        sparse_runs<32, FWD>(mine, lane, nodes, lmax);
+    else
+        dense_runs<FWD>(mine, lane, nodes, lmax);
+    if (last_zero) hist_add(mine, 1, lane, 1);
     // ---- bucket merge (see the header): wpl = sum of internal node weights.
     if (lane >= nb) nodes = 1;  // past the tail: nothing to do
     const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [w*64]
@@ -595,13 +665,29 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
         cur = nxt + carry;
     }
     }
-    }
-    if (!dma_issued) {  // the histogram paths used the stage until now
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): their bucket reads are done
-        __builtin_amdgcn_wave_barrier();
-        next_tile();
-    }
+    // the histogram paths used the stage until now
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): their bucket reads are done
+    __builtin_amdgcn_wave_barrier();
+    next_tile();
     return 8u * count + wpl;
+}
+
+// One tile in the wave's stage (Huffman layout, blocks past the end zeroed): the
+// bit count of every lane's block.  next_tile() is called once the stage may be
+// overwritten (the next tile's DMA, or nothing).
+template <bool FWD = false, typename NextTile>
+__device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, int wv, int nb, NextTile next_tile) {
+    const TileClass cl = classify<FWD>(mine, lane, nb);
+#ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
+    next_tile();
+    return cl.nz + cl.span;
+#endif
+    if (cl.narrow) {
+        NarrowLeaves L;
+        narrow_leaves<FWD>(mine, ctr, lane, wv, cl.vmin, cl.span, cl.last_zero, next_tile, L);  // the zero leaf included
+        return 8u * L.count + narrow_merge(L, wv);
+    }
+    return sort_tile_bits<FWD>(mine, lane, nb, cl, next_tile);
 }
 
 #ifndef DCTQ_HP_DIRECT
@@ -629,6 +715,10 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
     __syncthreads();
     const long long stride = (long long)gridDim.x * kHufWaves;
     long long t = (long long)blockIdx.x * kHufWaves + wv;
+    auto store_bits = [&](uint32_t out, long long tt, int n) {
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(bits + tt * 64, (short)0, n * 4, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
+    };
     if (t < ntiles) tile_dma(coef, t, nblk, mine, lane);
     for (; t < ntiles; t += stride) {
         const long long left = nblk - t * 64;
@@ -645,12 +735,10 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
             __builtin_amdgcn_s_waitcnt(0xC07F);
             __builtin_amdgcn_wave_barrier();
         }
-        const uint32_t out = tile_bits(mine, ctr, lane, wv, nb, [&] {
+        auto next_tile = [&] {
             if (t + stride < ntiles) tile_dma(coef, t + stride, nblk, mine, lane);
-        });
-        const __amdgpu_buffer_rsrc_t rb =
-            __builtin_amdgcn_make_buffer_rsrc(bits + t * 64, (short)0, nb * 4, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
+        };
+        store_bits(tile_bits(mine, ctr, lane, wv, nb, next_tile), t, nb);
     }
 }
 
