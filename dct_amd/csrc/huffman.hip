@@ -438,31 +438,60 @@ __device__ __forceinline__ uint32_t narrow_merge(const NarrowLeaves &L, int wv) 
     for (int w = 1; w <= 16; ++w) s3 += cnt[w];
     return s3;
 #endif
-    uint32_t p = 0, pm = 0;  // the pending node's weight (0: none); pending-merge nodes (bit = weight)
-    uint32_t qn = 0, qs = 0, qmn = 0xFFu, qmx = 0;  // heavy pairs (weights 2w, w = 9..16, ascending)
-    uint32_t wpl = 0;
-#pragma unroll
-    for (uint32_t w = 1; w <= 16; ++w) {
+    // p: the pending node's weight (0: none); pm: pending-merge nodes (bit = weight);
+    // qp: pairs of w = 9..16 (weight 2w > 16, at most 3 per w because node weights
+    // add up to <= 65) as 2-bit fields at 2 (w - 9), qs: their weights.
+    // WPL = the sum of the internal nodes' weights = the sum of every node's weight
+    // but the root's (each non-root node is a child of exactly one internal node),
+    // so it needs no per-merge accounting: acc sums the nodes of every light bucket,
+    // hs the heavy ones, fin the nodes of the closed-form finish, and the root
+    // weighs `count`.
+    uint32_t p = 0, pm = 0, acc = 0, qp = 0, qs = 0;
+    // v_mad_u32_u24 with the bucket's weight as an inline constant: LLVM turns
+    // (c & 1) * w into a compare and a select and c * w into v_mul_lo_u32 for
+    // some w (it cannot see that c < 2^24)
+    auto mad24 = [](uint32_t a, auto wc, uint32_t c) {
+        uint32_t d;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "n"(decltype(wc)::value), "v"(c));
+        return d;
+    };
+    auto bucket = [&](auto wc) {
+        constexpr uint32_t w = decltype(wc)::value;
         uint32_t c = cnt[w];
-        if (w >= 3) c += (pm >> w) & 1u;  // p + w' >= 3
-        const bool mp = p != 0 && c != 0;  // the pending node merges with one node of bucket w
-        const uint32_t nw = p + w;         // in (w, 2w): at most 31
-        wpl += mp ? nw : 0u;
+        if constexpr (w >= 3) c += (pm >> w) & 1u;  // p + w' >= 3
+        acc = mad24(c, wc, acc);                   // bucket w's nodes
+        const bool mp = min(p, c) != 0u;           // the pending node merges with one node of bucket w
         c -= mp ? 1u : 0u;
-        pm |= mp ? 1u << nw : 0u;
-        p = mp ? 0u : p;
+        pm |= mp ? (1u << w) << p : 0u;            // the merged node: weight p + w in (w, 2w), at most 31
+        p = mad24(c & 1u, wc, mp ? 0u : p);        // c odd: one node of w waits (p was 0 or merged)
         const uint32_t pairs = c >> 1;
-        wpl += pairs * 2 * w;
-        if (2 * w <= 16) {
+        if constexpr (2 * w <= 16) {
             cnt[2 * w] += pairs;
         } else {
-            qn += pairs;
-            qs += pairs * 2 * w;
-            qmn = (pairs && qmn == 0xFFu) ? 2 * w : qmn;
-            qmx = pairs ? 2 * w : qmx;
+            qp |= pairs << (2 * (w - 9));
+            qs = mad24(pairs, std::integral_constant<uint32_t, 2 * w>{}, qs);
         }
-        p = (c & 1u) ? w : p;
-    }
+    };
+    bucket(std::integral_constant<uint32_t, 1>{});
+    bucket(std::integral_constant<uint32_t, 2>{});
+    bucket(std::integral_constant<uint32_t, 3>{});
+    bucket(std::integral_constant<uint32_t, 4>{});
+    bucket(std::integral_constant<uint32_t, 5>{});
+    bucket(std::integral_constant<uint32_t, 6>{});
+    bucket(std::integral_constant<uint32_t, 7>{});
+    bucket(std::integral_constant<uint32_t, 8>{});
+    bucket(std::integral_constant<uint32_t, 9>{});
+    bucket(std::integral_constant<uint32_t, 10>{});
+    bucket(std::integral_constant<uint32_t, 11>{});
+    bucket(std::integral_constant<uint32_t, 12>{});
+    bucket(std::integral_constant<uint32_t, 13>{});
+    bucket(std::integral_constant<uint32_t, 14>{});
+    bucket(std::integral_constant<uint32_t, 15>{});
+    bucket(std::integral_constant<uint32_t, 16>{});
+    // the heavy pairs: count, min, max
+    const uint32_t qn = (uint32_t)__builtin_popcount(qp & 0x5555u) + 2u * (uint32_t)__builtin_popcount(qp & 0xAAAAu);
+    const uint32_t qmn = qp ? 18u + 2u * ((uint32_t)__builtin_ctz(qp) >> 1) : 0xFFu;
+    const uint32_t qmx = qp ? 18u + 2u * ((31u - (uint32_t)__builtin_clz(qp)) >> 1) : 0u;
     // the pending-merge nodes above 16 (<= 3 bits of pm, bits 17..31)
     {
         uint32_t b = pm & ~0x1FFFFu;
@@ -483,7 +512,7 @@ __device__ __forceinline__ uint32_t narrow_merge(const NarrowLeaves &L, int wv) 
     } else {
         fin = hn == 3 ? 2 * (h1 + h2) + h3 : hn == 2 ? h1 + h3 : 0u;
     }
-    return wpl + fin;
+    return acc + hs + fin - L.count;
 }
 
 #ifndef DCTQ_HUF_BITS_AUX

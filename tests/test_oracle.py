@@ -239,66 +239,66 @@ def test_huffman_bucket_model_is_exact():
 
 def register_merge_wpl(freqs):
     """Python model of the narrow path's register merge (dct_amd/csrc/huffman.hip,
-    narrow_tile), operation for operation:
+    narrow_merge), operation for operation:
       * leaf weights <= 16 counted in 16 buckets; the bucket merge scans w = 1..16
         (a pending node merges with one node of the next non-empty bucket, the rest
         pair up);
       * a pending merge makes ONE node of weight p + w in (w, 2w), and successive
         ones are strictly heavier, so they are bits of a mask (bit p + w), never
         two in one bucket;
-      * every node heavier than 16 -- leaves, pairs of w >= 9, pending merges --
-        waits aside.  All node weights add up to the symbol count (<= 65), so there
-        are at most 3 of them, and their count, sum, min and max give them sorted;
-      * the pending node (<= 16, the lightest) and those finish in closed form.
-    Returns the weighted path length (sum of internal node weights)."""
+      * every node heavier than 16 -- leaves, pairs of w >= 9 (at most 3 per w, kept
+        as 2-bit fields), pending merges -- waits aside.  All node weights add up to
+        the symbol count (<= 65), so there are at most 3 of them, and their count,
+        sum, min and max give them sorted;
+      * the pending node (<= 16, the lightest) and those finish in closed form;
+      * the WPL (sum of internal node weights) is the sum of EVERY node's weight but
+        the root's (each non-root node is a child of exactly one internal node): the
+        nodes of each light bucket (acc), the heavy nodes (hs), the internal nodes of
+        the closed-form finish (fin), minus the root (the symbol count).
+    Returns the weighted path length."""
     cnt = [0] * 17
-    hn, hs, hmn, hmx = 0, 0, 99, 0  # heavy nodes: count, sum, min, max
-
-    def heavy(k, x):
-        nonlocal hn, hs, hmn, hmx
-        if k:
-            hn, hs, hmn, hmx = hn + k, hs + k * x, min(hmn, x), max(hmx, x)
-
+    hn, hs, hmn, hmx = 0, 0, 0xFF, 0  # heavy nodes: count, sum, min, max
     for f in freqs:
         if f > 16:
-            heavy(1, f)
+            hn, hs, hmn, hmx = hn + 1, hs + f, min(hmn, f), max(hmx, f)
         else:
             cnt[f] += 1
-    wpl, p, pm = 0, 0, 0
+    p = pm = acc = qp = qs = 0
     for w in range(1, 17):
-        c = cnt[w] + ((pm >> w) & 1)
-        if p and c:
-            wpl += p + w
-            pm |= 1 << (p + w)
-            c -= 1
-            p = 0
+        c = cnt[w] + (((pm >> w) & 1) if w >= 3 else 0)
+        acc += c * w  # bucket w's nodes
+        mp = min(p, c) != 0  # the pending node merges with one node of bucket w
+        c -= 1 if mp else 0
+        pm |= (1 << w) << p if mp else 0
+        p = (0 if mp else p) + (c & 1) * w
         pairs = c >> 1
-        wpl += pairs * 2 * w
         if 2 * w <= 16:
             cnt[2 * w] += pairs
         else:
-            heavy(pairs, 2 * w)
-        if c & 1:
-            p = w
-    for b in range(17, 32):
-        heavy((pm >> b) & 1, b)
+            assert pairs <= 3
+            qp |= pairs << (2 * (w - 9))
+            qs += pairs * 2 * w
+    pc = lambda x: bin(x).count("1")  # noqa: E731
+    qn = pc(qp & 0x5555) + 2 * pc(qp & 0xAAAA)
+    qmn = 18 + 2 * (((qp & -qp).bit_length() - 1) >> 1) if qp else 0xFF
+    qmx = 18 + 2 * ((qp.bit_length() - 1) >> 1) if qp else 0
+    b = pm & ~0x1FFFF  # pending merges above 16: <= 3 bits
+    n = pc(b)
+    lo = (b & -b).bit_length() - 1 if b else 0xFF
+    hi = b.bit_length() - 1 if b else 0
+    mid = ((b & (b - 1)) & -(b & (b - 1))).bit_length() - 1 if n == 3 else 0
+    hn += n + qn
+    hs += (lo if n else 0) + (mid if n == 3 else 0) + (hi if n >= 2 else 0) + qs
+    hmn, hmx = min(hmn, qmn, lo), max(hmx, qmx, hi)
     assert hn <= 3, hn
     h1, h3 = hmn, hmx
     h2 = hs - h1 - h3 if hn == 3 else h3
-    if p:
-        if hn == 3:
-            s = p + h1
-            wpl += 2 * s + 2 * h2 + h3 + min(s, h3)
-        elif hn == 2:
-            wpl += 2 * (p + h1) + h2
-        elif hn == 1:
-            wpl += p + h1
+    if p:  # p < 17 <= h1: nodes p, h1, h2, h3
+        s = p + h1
+        fin = 2 * s + 2 * h2 + h3 + min(s, h3) if hn == 3 else 2 * s + h2 if hn == 2 else s if hn == 1 else 0
     else:
-        if hn == 3:
-            wpl += 2 * (h1 + h2) + h3
-        elif hn == 2:
-            wpl += h1 + h3
-    return wpl
+        fin = 2 * (h1 + h2) + h3 if hn == 3 else h1 + h3 if hn == 2 else 0
+    return acc + hs + fin - sum(freqs)
 
 
 def test_huffman_register_merge_model_is_exact():
