@@ -129,11 +129,12 @@ __device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine,
                                              uint32_t &lmax) {
     // branch-free: every element adds (end ? 1 : 0) at its run length, so no
     // per-element exec mask is live (64 of them spilled to SGPR lanes)
+    // a[] is sorted with kSent (max) last: a run ends where the next key differs,
+    // and a kSent run is never one (the element after a kSent is kSent)
     uint32_t run = 1;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const uint32_t nxt = i + 1 < N ? a[i + 1 < N ? i + 1 : N - 1] : kSent;
-        const uint32_t end = a[i] != kSent && nxt != a[i] ? 1u : 0u;
+        const uint32_t end = (i + 1 < N ? a[i] != a[i + 1 < N ? i + 1 : N - 1] : a[i] != kSent) ? 1u : 0u;
         hist_add(mine, run, lane, end);
         if (kMax) lmax = end && run > lmax ? run : lmax;
         nodes += end;
@@ -217,21 +218,45 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
     tile_row<FWD>(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
     __builtin_amdgcn_wave_barrier();
-    // branch-free compaction: every key is written at the next slot, which advances
-    // only past a nonzero (a zero's write is overwritten or lies past `pos`)
+    // branch-free compaction: every value is written at the next slot, which advances
+    // only past a nonzero (a zero's write is overwritten or lies past `pos`).  The
+    // key is the value's raw 16 bits (zeros never reach the sort, and any injective
+    // key groups equal values): ds_write_b16 / ds_write_b16_d16_hi straight from the
+    // packed pair, and one packed min gives both nonzero flags.
     uint32_t pos = 0;
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        const uint32_t v = key_of(d, i);
-        *reinterpret_cast<uint32_t *>(mine + (pos * 64 + lane) * 4) = v;
-        pos += v != kSent ? 1u : 0u;
-    }
-    __builtin_amdgcn_wave_barrier();
     uint32_t b[N];
+    if constexpr (!FWD) {
+        const uint32_t one2 = 0x00010001u;
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-        const uint32_t v = *reinterpret_cast<const uint32_t *>(mine + (k * 64 + lane) * 4);
-        b[k] = (uint32_t)k < pos ? v : kSent;
+        for (int h = 0; h < 32; ++h) {
+            uint32_t nz2;  // (lo != 0, hi != 0) as 16-bit halves; inline asm: LLVM expands the packed min
+            asm volatile("v_pk_min_u16 %0, %1, %2" : "=v"(nz2) : "v"(d[h]), "v"(one2));
+            *reinterpret_cast<uint16_t *>(mine + (pos * 64 + lane) * 4) = (uint16_t)d[h];
+            pos += nz2 & 0xFFFFu;
+            *reinterpret_cast<uint16_t *>(mine + (pos * 64 + lane) * 4) = (uint16_t)(d[h] >> 16);
+            pos += nz2 >> 16;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const uint32_t v = *reinterpret_cast<const uint16_t *>(mine + (k * 64 + lane) * 4);
+            b[k] = (uint32_t)k < pos ? v : kSent;
+        }
+    } else {
+        // the fused kernel (huffman_from_pixels) keeps 32-bit keys: with the 16-bit
+        // stores its loop invariants spilled (12-14 VGPRs at its 168-register bound)
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            const uint32_t v = key_of(d, i);
+            *reinterpret_cast<uint32_t *>(mine + (pos * 64 + lane) * 4) = v;
+            pos += v != kSent ? 1u : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const uint32_t v = *reinterpret_cast<const uint32_t *>(mine + (k * 64 + lane) * 4);
+            b[k] = (uint32_t)k < pos ? v : kSent;
+        }
     }
     sort_net<N>(b);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): column reads done before the histogram overwrites them
