@@ -102,10 +102,15 @@ __device__ __forceinline__ void hist_add(char *h, int w, int lane, uint32_t n) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-// zero the wave's histogram (9 KiB: buckets 0..64)
+// zero buckets 0..8 * CHUNKS - 1 of the wave's histogram (1 KiB = 8 buckets per
+// ds_write_b128): every weight of a block of S symbols is at most S, and the
+// merge reads one bucket past the last it processes, so S + 2 buckets suffice --
+// 3 chunks for the 16-nonzero path (S <= 17), 5 for the 32 one, 9 (all 65) dense
+template <int CHUNKS>
 __device__ __forceinline__ void hist_zero(char *mine, int lane) {
+    static_assert(CHUNKS >= 1 && CHUNKS <= 9, "the histogram has 65 buckets of 128 B");
 #pragma unroll
-    for (int k = 0; k < 9; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < CHUNKS; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
 }
 
 // Occupancy of the lane's histogram: bit w-1 set while bucket w may hold nodes
@@ -261,7 +266,7 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
     sort_net<N>(b);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): column reads done before the histogram overwrites them
     __builtin_amdgcn_wave_barrier();
-    hist_zero(mine, lane);
+    hist_zero<(N + 1 + 2 + 7) / 8>(mine, lane);  // S <= N + 1 symbols: buckets 0..S + 1
     __builtin_amdgcn_wave_barrier();
     runs_to_hist<N, false>(b, mine, lane, nodes, lmax);
 }
@@ -281,7 +286,7 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
     sort_net<64>(a);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile reads are done before the histogram overwrites them
     __builtin_amdgcn_wave_barrier();
-    hist_zero(mine, lane);
+    hist_zero<9>(mine, lane);
     __builtin_amdgcn_wave_barrier();
     runs_to_hist<64, true>(a, mine, lane, nodes, lmax);
 }
