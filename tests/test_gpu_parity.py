@@ -1028,6 +1028,55 @@ def test_huffman_bits_golden_and_planes(T, dm):
         assert np.array_equal(got, O.huffman_bits_plane(c))
 
 
+def test_huffman_bits_frequency_shapes(T, dm):
+    """The register merge on the shapes its closed form and masks must handle, through every path:
+    blocks built from frequency partitions (tests/test_oracle.py::register_merge_wpl's generator)
+    -- light leaves only, one to three leaves heavier than 16 (the weight rows read with the light
+    ones, 17..20, and the rows read one by one, 21..64), pending merges above 16 -- laid out as
+    dense tiles of span < 64 (the narrow counting path), as <= 32-nonzero tiles (the sparse sort
+    paths) and as wide dense tiles (the 64-network), each block against the oracle."""
+    import oracle as O
+    rng = np.random.default_rng(2024)
+
+    def partition(total, heavy):
+        f = list(heavy)
+        left = total - sum(f)
+        while left:
+            x = int(min(left, rng.choice([1, 1, 2, 3, 4, 5, 8, 16])))
+            f.append(x)
+            left -= x
+        return f
+
+    def block(freqs, base, zeros_last):
+        vals = [base + i for i, x in enumerate(freqs) for _ in range(x)]
+        b = np.zeros(64, np.int16)
+        pos = rng.permutation(63 if zeros_last else 64)[:len(vals)]
+        b[pos] = vals
+        return b
+
+    heavies = [(), (17,), (20,), (21,), (30,), (17, 17), (20, 25), (17, 18, 19), (21, 21, 21), (40,), (64,),
+               (33, 31), (18, 22, 23)]
+    narrow, sparse, wide = [], [], []
+    for r in range(64 * 6):
+        h = heavies[r % len(heavies)]
+        total = 64 if sum(h) < 64 or rng.random() < 0.5 else sum(h)
+        f = partition(total, h)
+        if len(f) > 63:
+            f = f[:63]
+        nb = block(f, int(rng.integers(-40, 2)), zeros_last=False)  # values in a window of <= 63: narrow
+        nb[nb == 0] = 1 if (nb == 0).all() else nb[nb != 0][0]  # no zeros: the span stays that of the values
+        narrow.append(nb)
+        hs = [x for x in h if x <= 32][:1]
+        fs = partition(int(rng.integers(sum(hs) if hs else 1, 33)), hs)
+        sparse.append(block(fs, 1 + int(rng.integers(0, 50)), zeros_last=bool(rng.random() < 0.5)))
+        w = block(f, -200, zeros_last=False)
+        w[int(rng.integers(64))] = 300  # span > 64: the sort path
+        wide.append(w)
+    for c in (np.array(narrow), np.array(sparse), np.array(wide)):
+        got = dm.huffman_bits(T.from_numpy(c).cuda()).cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, O.huffman_bits_plane(c))
+
+
 def test_huffman_bits_large_plane(T, dm):
     """A 4K luma frame stack (several tiles per wave in the grid-stride loop) + 5 ragged
     blocks, every block against the oracle; invalid arguments rejected."""
