@@ -329,7 +329,9 @@ __device__ __forceinline__ void narrow_leaves(const char *mine, char *ctr, int l
     next_tile();
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     const uint32_t base = (uint32_t)(lane * 4);  // byte 0 of the lane's dword in every row
-    const uint32_t sh = 8u * (uint32_t)wv, inc = 1u << sh, keep = ~(0xFFu << sh);  // the wave's byte of it
+    const uint32_t sh = 8u * (uint32_t)wv, inc = 1u << sh;  // the wave's byte of it
+    uint32_t keep = ~(0xFFu << sh);
+    asm volatile("" : "+v"(keep));  // rematerialised per tile: hoisted out of the kernel loop, the fused kernel spilled it
     const u16x2 off = {(unsigned short)(-vmin), (unsigned short)(-vmin)};
     auto at = [&](uint32_t row) { return reinterpret_cast<uint32_t *>(ctr + (row << 8) + base); };
     auto take_raw = [&](uint32_t row) {  // row's dword, the wave's byte cleared in LDS
