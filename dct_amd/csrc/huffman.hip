@@ -59,7 +59,8 @@ constexpr int kHufThreads = 64 * kHufWaves;
 // ds_read_b128 of tile_row conflict-free (each 16-lane group of a b128 read
 // covers 16 distinct 16-B bank groups) with no padding, so the tile can arrive
 // by LDS-DMA (1 KiB contiguous per instruction; each lane picks its source piece).
-// 9 KiB per wave: the dense/sparse paths reuse it for their histogram (kHistBytes).
+// 9 KiB per wave: the sparse paths reuse it for their compacted keys (up to 33 slots
+// of 256 B), huffman_from_pixels for the forward's stage (64 x kPitch2 + 128 B).
 constexpr int kHufWaveLds = 9 * 1024;
 // The narrow path's value counters and weight histogram, one region shared by
 // the workgroup's waves: byte  row * 256 + lane * 4 + wave  is wave `wave`'s
@@ -90,28 +91,26 @@ __device__ __forceinline__ void sort_net(uint32_t (&a)[N]) {
                     if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) cas(a[i + j], a[i + j + k]);
 }
 
-// Histogram column of `lane`: 16-bit counter of weight w (0..64) at byte
-// w*128 + lane*2 (dword w*32 + lane/2: lanes 2q, 2q+1 share a dword, bank q --
-// conflict-free for any mix of weights across lanes).  Bucket 0 is a dummy that
-// absorbs "no leaf" adds, so the count loops stay branch-free.  65 buckets =
-// 8 320 B, inside the wave's 9 KiB tile stage.
-constexpr int kHistBytes = 65 * 128;
-static_assert(kHistBytes <= kHufWaveLds, "the histogram fits the wave's tile stage");
-__device__ __forceinline__ void hist_add(char *h, int w, int lane, uint32_t n) {
-    __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(h + w * 128 + (lane & ~1) * 2), n << (16 * (lane & 1)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
-// zero buckets 0..8 * CHUNKS - 1 of the wave's histogram (1 KiB = 8 buckets per
-// ds_write_b128): every weight of a block of S symbols is at most S, and the
-// merge reads one bucket past the last it processes, so S + 2 buckets suffice --
-// 3 chunks for the 16-nonzero path (S <= 17), 5 for the 32 one, 9 (all 65) dense
-template <int CHUNKS>
-__device__ __forceinline__ void hist_zero(char *mine, int lane) {
-    static_assert(CHUNKS >= 1 && CHUNKS <= 9, "the histogram has 65 buckets of 128 B");
-#pragma unroll
-    for (int k = 0; k < CHUNKS; ++k) *reinterpret_cast<uint4 *>(mine + k * 1024 + lane * 16) = make_uint4(0, 0, 0, 0);
-}
+// The sparse and dense paths' weight histogram lives in the workgroup's shared
+// byte region (kHufCtrBytes), like the narrow path's counters: byte
+// w * 256 + lane * 4 + wave is the wave's count of nodes of weight w (<= 65) for
+// that lane -- conflict-free, and the tile stage is free for the next tile's DMA as
+// soon as the row (or the compacted keys) are in registers.  Every bucket is read
+// AND cleared when the merge processes it, so the region stays zeroed between tiles.
+struct Hist {
+    char *ctr;
+    uint32_t base, sh;  // lane * 4, 8 * wave
+    __device__ __forceinline__ uint32_t *at(uint32_t w) const { return reinterpret_cast<uint32_t *>(ctr + (w << 8) + base); }
+    __device__ __forceinline__ void add(uint32_t w, uint32_t n) const {
+        __hip_atomic_fetch_add(at(w), n << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __device__ __forceinline__ uint32_t peek(uint32_t w) const { return (*at(w) >> sh) & 0xFFu; }
+    __device__ __forceinline__ uint32_t take(uint32_t w) const {  // read and clear the wave's byte
+        uint32_t keep = ~(0xFFu << sh);
+        asm volatile("" : "+v"(keep));  // rematerialised per use (a hoisted copy spills in the fused kernel)
+        return (__hip_atomic_fetch_and(at(w), keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFu;
+    }
+};
 
 // Occupancy of the lane's histogram: bit w-1 set while bucket w may hold nodes
 // (the merge jumps from one occupied bucket to the next).
@@ -130,7 +129,7 @@ __device__ __forceinline__ uint32_t key_of(const uint32_t (&d)[32], int i) {
 // Runs of equal values in the sorted registers -> one histogram count per
 // distinct value at its frequency; `nodes` += distinct values.
 template <int N, bool kMax>
-__device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine, int lane, uint32_t &nodes,
+__device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], const Hist &h, uint32_t &nodes,
                                              uint32_t &lmax) {
     // branch-free: every element adds (end ? 1 : 0) at its run length, so no
     // per-element exec mask is live (64 of them spilled to SGPR lanes)
@@ -140,7 +139,7 @@ __device__ __forceinline__ void runs_to_hist(const uint32_t (&a)[N], char *mine,
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const uint32_t end = (i + 1 < N ? a[i] != a[i + 1 < N ? i + 1 : N - 1] : a[i] != kSent) ? 1u : 0u;
-        hist_add(mine, run, lane, end);
+        h.add(run, end);
         if (kMax) lmax = end && run > lmax ? run : lmax;
         nodes += end;
         run = end ? 1u : run + 1u;
@@ -217,8 +216,9 @@ __device__ __forceinline__ void tile_dma(const int16_t *coef, long long t, long 
 // Each path re-reads the tile row itself, so nothing but scalars is live across
 // the path choice and each path gets its own register allocation (a shared
 // 32-register row made the compiler hold 188-336 VGPRs).
-template <int N, bool FWD = false>
-__device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &nodes, uint32_t &lmax) {
+template <int N, bool FWD = false, typename NextTile>
+__device__ __forceinline__ void sparse_runs(char *mine, const Hist &h, int lane, uint32_t &nodes, uint32_t &lmax,
+                                            NextTile next_tile) {
     uint32_t d[32];
     tile_row<FWD>(mine, lane, d);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
@@ -263,16 +263,16 @@ __device__ __forceinline__ void sparse_runs(char *mine, int lane, uint32_t &node
             b[k] = (uint32_t)k < pos ? v : kSent;
         }
     }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the keys are in registers, the stage is free
+    __builtin_amdgcn_wave_barrier();
+    next_tile();
     sort_net<N>(b);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): column reads done before the histogram overwrites them
-    __builtin_amdgcn_wave_barrier();
-    hist_zero<(N + 1 + 2 + 7) / 8>(mine, lane);  // S <= N + 1 symbols: buckets 0..S + 1
-    __builtin_amdgcn_wave_barrier();
-    runs_to_hist<N, false>(b, mine, lane, nodes, lmax);
+    runs_to_hist<N, false>(b, h, nodes, lmax);
 }
 
-template <bool FWD = false>
-__device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes, uint32_t &lmax) {
+template <bool FWD = false, typename NextTile>
+__device__ __forceinline__ void dense_runs(char *mine, const Hist &h, int lane, uint32_t &nodes, uint32_t &lmax,
+                                           NextTile next_tile) {
     uint32_t a[64];
     {
         uint32_t d[32];
@@ -283,12 +283,11 @@ __device__ __forceinline__ void dense_runs(char *mine, int lane, uint32_t &nodes
             a[2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
         }
     }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the row is in registers, the stage is free
+    __builtin_amdgcn_wave_barrier();
+    next_tile();
     sort_net<64>(a);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the tile reads are done before the histogram overwrites them
-    __builtin_amdgcn_wave_barrier();
-    hist_zero<9>(mine, lane);
-    __builtin_amdgcn_wave_barrier();
-    runs_to_hist<64, true>(a, mine, lane, nodes, lmax);
+    runs_to_hist<64, true>(a, h, nodes, lmax);
 }
 
 // Tiles whose every block's values (zeros included) span fewer than 64 integers
@@ -627,11 +626,14 @@ __device__ __forceinline__ TileClass classify(const char *mine, int lane, int nb
 }
 
 // The sparse and dense paths of a tile that is not narrow: runs of equal values
-// -> histogram of frequencies in the wave's stage, then the bucket merge; calls
-// next_tile() once the stage is free.  Returns the bit counts.
+// -> histogram of frequencies in the shared byte region (Hist), then the bucket
+// merge; they call next_tile() as soon as the stage is free (keys or row in
+// registers), so the next tile's DMA overlaps the sort and the merge.  Returns the
+// bit counts.
 template <bool FWD = false, typename NextTile>
-__device__ __forceinline__ uint32_t sort_tile_bits(char *mine, int lane, int nb, const TileClass &cl,
-                                                   NextTile next_tile) {
+__device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int lane, int wv, int nb,
+                                                   const TileClass &cl, NextTile next_tile) {
+    const Hist h{ctr, (uint32_t)(lane * 4), 8u * (uint32_t)wv};
     const uint32_t nz = cl.nz;
     const bool last_zero = cl.last_zero;
     uint32_t count = nz + (last_zero ? 1u : 0u);  // symbols: the nonzeros, plus a 0 once if c[63] == 0
@@ -645,40 +647,40 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, int lane, int nb,
 #endif
     uint32_t wpl = 0, pending = 0;
     if (!__builtin_amdgcn_ballot_w64(nz > 16))
-        sparse_runs<16, FWD>(mine, lane, nodes, lmax);
+        sparse_runs<16, FWD>(mine, h, lane, nodes, lmax, next_tile);
     else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-        sparse_runs<32, FWD>(mine, lane, nodes, lmax);
+        sparse_runs<32, FWD>(mine, h, lane, nodes, lmax, next_tile);
     else
-        dense_runs<FWD>(mine, lane, nodes, lmax);
-    if (last_zero) hist_add(mine, 1, lane, 1);
-    // ---- bucket merge (see the header): wpl = sum of internal node weights.
-    if (lane >= nb) nodes = 1;  // past the tail: nothing to do
-    const uint16_t *bucket = reinterpret_cast<const uint16_t *>(mine + lane * 2);  // weight w at [w*64]
+        dense_runs<FWD>(mine, h, lane, nodes, lmax, next_tile);
+    if (last_zero) h.add(1, 1);
+    // ---- bucket merge (see the header): wpl = sum of internal node weights.  Lanes
+    // past the tail hold one leaf (the zero block's last 0) and run as any other,
+    // so their bucket is cleared too.
     if (lane_merge) {
         // occupancy of the leaf buckets, read back up to the wave's largest leaf weight
         // (cheaper than marking every leaf; this wave's LDS atomics are already ordered)
         uint64_t occ = 0;
 #pragma unroll
         for (uint32_t w = 1; w <= 8; ++w)  // independent reads, in flight together
-            occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
+            occ |= h.peek(w) ? 1ull << (w - 1) : 0ull;
         for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w)
-            occ |= bucket[w * 64] ? 1ull << (w - 1) : 0ull;
-        if (lane >= nb) occ = 0;  // past the tail (the narrow path keeps them: it must clear its rows)
+            occ |= h.peek(w) ? 1ull << (w - 1) : 0ull;
         // Each lane jumps to its own next occupied bucket (lowest bit of occ), so the
         // loop runs as many steps as the busiest lane has occupied buckets, not up to
         // its largest weight.  New weights (pending + w, 2w) are above w, so the scan
         // order is the bucket order; weights never exceed the symbol count (<= 64).
         // The lane is done when no bucket is left: its last node (the root) is then
-        // `pending`.  The step cap only bounds the loop.
+        // `pending`, and every bucket it held nodes in was taken (cleared).  The step
+        // cap only bounds the loop.
         for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ != 0); ++step) {
             if (occ) {
                 const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
                 occ &= occ - 1ull;  // bucket w is emptied by this step
-                uint32_t c = bucket[w * 64];
+                uint32_t c = h.take(w);
                 if (pending && c) {
                     const uint32_t nw = pending + w;
                     wpl += nw;
-                    hist_add(mine, nw, lane, 1);
+                    h.add(nw, 1);
                     mark(occ, nw, 1);
                     --c;
                     pending = 0;
@@ -686,50 +688,49 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, int lane, int nb,
                 const uint32_t pairs = c >> 1;
                 if (pairs) {
                     wpl += pairs * 2 * w;
-                    hist_add(mine, 2 * w, lane, pairs);
+                    h.add(2 * w, pairs);
                     mark(occ, 2 * w, 1);
                 }
                 if (c & 1) pending = w;
             }
         }
     } else {
-    // Sparse tiles (few weights): every weight in turn; bucket w+1 is read at the top of iteration w, so its
-    // LDS latency hides behind the iteration; the only merges of iteration w that
-    // land on w+1 (pending 1 + w, and the pairs of w = 1) are carried in a register
-    uint32_t cur = bucket[64];
-    for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
-        const uint32_t nxt = w < 64 ? bucket[(w + 1) * 64] : 0u;
-        uint32_t c = cur, carry = 0;
-        if (nodes > 1) {
-            if (pending && c) {
-                const uint32_t nw = pending + w;
-                wpl += nw;
-                if (nw == w + 1)
-                    carry = 1;
-                else
-                    hist_add(mine, nw, lane, 1);
-                --c;
-                --nodes;
-                pending = 0;
+        // Sparse tiles (few weights): every weight in turn; bucket w+1 is taken at the
+        // top of iteration w, so its LDS latency hides behind the iteration; the only
+        // merges of iteration w that land on w+1 (pending 1 + w, and the pairs of
+        // w = 1) are carried in a register.  A lane stops once its root is made; the
+        // root's bucket (weight = count) may then be left, and is cleared after the loop.
+        uint32_t cur = h.take(1);
+        for (uint32_t w = 1; w <= 64 && __builtin_amdgcn_ballot_w64(nodes > 1); ++w) {
+            const uint32_t nxt = w < 64 ? h.take(w + 1) : 0u;
+            uint32_t c = cur, carry = 0;
+            if (nodes > 1) {
+                if (pending && c) {
+                    const uint32_t nw = pending + w;
+                    wpl += nw;
+                    if (nw == w + 1)
+                        carry = 1;
+                    else
+                        h.add(nw, 1);
+                    --c;
+                    --nodes;
+                    pending = 0;
+                }
+                const uint32_t pairs = c >> 1;
+                if (pairs) {
+                    wpl += pairs * 2 * w;
+                    nodes -= pairs;
+                    if (w == 1)
+                        carry += pairs;
+                    else
+                        h.add(2 * w, pairs);
+                }
+                if (c & 1) pending = w;
             }
-            const uint32_t pairs = c >> 1;
-            if (pairs) {
-                wpl += pairs * 2 * w;
-                nodes -= pairs;
-                if (w == 1)
-                    carry += pairs;
-                else
-                    hist_add(mine, 2 * w, lane, pairs);
-            }
-            if (c & 1) pending = w;
+            cur = nxt + carry;
         }
-        cur = nxt + carry;
+        (void)h.take(count);  // the root, or a lone leaf, if still stored
     }
-    }
-    // the histogram paths used the stage until now
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): their bucket reads are done
-    __builtin_amdgcn_wave_barrier();
-    next_tile();
     return 8u * count + wpl;
 }
 
@@ -748,7 +749,7 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
         narrow_leaves<FWD>(mine, ctr, lane, wv, cl.vmin, cl.span, cl.last_zero, next_tile, L);  // the zero leaf included
         return 8u * L.count + narrow_merge(L, wv);
     }
-    return sort_tile_bits<FWD>(mine, lane, nb, cl, next_tile);
+    return sort_tile_bits<FWD>(mine, ctr, lane, wv, nb, cl, next_tile);
 }
 
 #ifndef DCTQ_HP_DIRECT
