@@ -27,16 +27,17 @@
 // orc_huffman_bits) and is pinned to the compiled reference; the GPU result is
 // compared with it (tests/test_gpu_parity.py::test_huffman_bits*).
 //
-// Layout: one LANE per block (64 blocks per wave).  The wave stages its tile
-// (8 KiB) in LDS with 1 KiB loads; each lane sorts its values with a Batcher
-// odd-even merge network in registers (equal values become adjacent; zeros map
-// to the top and are dropped) -- all 64, or, when every block of the tile has
-// at most 16 / 32 nonzero coefficients (natural content), just those, compacted
-// through LDS -- adds one count per run length into its column of an LDS
-// histogram (16-bit counters, two lanes per dword, ds_add_u32), then runs the
-// bucket merge.  Tiles whose every block's values span < 64 integers (q50
-// noise, most natural content) skip the sort: narrow_counts below.  VALU-bound
-// (DESIGN.md 3.8).
+// Layout: one LANE per block (64 blocks per wave).  The wave's tile (8 KiB)
+// arrives in LDS by LDS-DMA, the next one while the current one is processed.
+// Dense tiles whose every block's values span < 64 integers (q50 noise) count
+// their values in a workgroup-shared byte region and merge in registers
+// (narrow_leaves / narrow_merge).  Other tiles sort each lane's values with a
+// Batcher odd-even merge network in registers (equal values become adjacent;
+// zeros map to the top and are dropped) -- all 64, or, when every block of the
+// tile has at most 16 / 32 nonzero coefficients (natural content), just those,
+// compacted through LDS -- add one count per run length into the same shared
+// region (Hist), and run the bucket merge there.  VALU- and LDS-latency-bound
+// at 3 waves/SIMD.
 // DCTQ_HUF_MIN_WAVES (launch bound, default 3 waves/SIMD: 168 VGPRs) is an A/B knob.
 #include <type_traits>
 
@@ -62,8 +63,8 @@ constexpr int kHufThreads = 64 * kHufWaves;
 // 9 KiB per wave: the sparse paths reuse it for their compacted keys (up to 33 slots
 // of 256 B), huffman_from_pixels for the forward's stage (64 x kPitch2 + 128 B).
 constexpr int kHufWaveLds = 9 * 1024;
-// The narrow path's value counters and weight histogram, one region shared by
-// the workgroup's waves: byte  row * 256 + lane * 4 + wave  is wave `wave`'s
+// The narrow path's value counters and every path's weight histogram, one region
+// shared by the workgroup's waves: byte  row * 256 + lane * 4 + wave  is wave `wave`'s
 // 8-bit counter `row` of lane `lane` (counts never exceed 64).  Every lane owns
 // a dword per row (conflict-free banks), the wave owns a byte of it (its adds
 // are 1 << 8 * wave), and one v_perm builds a dword address from a value (byte
@@ -766,7 +767,7 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
 #endif
 __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                    uint32_t *__restrict__ bits, long long ntiles) {
-    // per wave: the tile stage (9 KiB), reused for the histogram; per workgroup: the narrow path's counters
+    // per wave: the tile stage (9 KiB), reused for the sparse keys; per workgroup: the counters and histograms
     __shared__ uint4 lds[kHufWaves * kHufWaveLds / 16];
     __shared__ uint4 ctr_lds[kHufCtrBytes / 16];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
