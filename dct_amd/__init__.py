@@ -61,6 +61,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
     if diagnostic:
         sig.update({
             "dctq_diag_plan_set_variant": ([vp, i], i),
+            "dctq_diag_plan_set_num_cus": ([vp, i], i),
             "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_rt_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_diag_stream": ([i, vp, vp, ll, vp], i),
@@ -158,18 +159,23 @@ class Plan:
     """Tables for one (quality, adaptive) configuration on the current device
     (quant_init(8, quality, adaptive) semantics, src/quantization.c:19-41)."""
 
-    def __init__(self, quality: int = 50, adaptive: bool = False, variant: int = None, diagnostic: bool = False):
+    def __init__(self, quality: int = 50, adaptive: bool = False, variant: int = None, diagnostic: bool = False,
+                 num_cus: int = None):
         """variant (tests / A/B only): force the forward kernel through the diagnostic
         library (dctq_diag_plan_set_variant: 1 = v1, 3 = v3 in-place ties, 4 = v2 tie
-        queue, at any size); diagnostic: create the plan in the diagnostic library
-        (needed for diag_movement_planes)."""
+        queue, at any size); num_cus (tests only): launch as if the device had that many
+        CUs (dctq_diag_plan_set_num_cus: smaller grids, more batches per wave);
+        diagnostic: create the plan in the diagnostic library (needed for
+        diag_movement_planes)."""
         self.quality, self.adaptive = quality, bool(adaptive)
-        self._L = diag() if (variant is not None or diagnostic) else lib()
+        self._L = diag() if (variant is not None or num_cus is not None or diagnostic) else lib()
         h = C.c_void_p()
         self._chk(self._L.dctq_plan_create(int(quality), int(bool(adaptive)), C.byref(h)))
         self._h = h
         if variant is not None:
             self._chk(self._L.dctq_diag_plan_set_variant(h, int(variant)))
+        if num_cus is not None:
+            self._chk(self._L.dctq_diag_plan_set_num_cus(h, int(num_cus)))
 
     def _chk(self, rc: int) -> None:
         _check(rc, self._L)

@@ -19,6 +19,12 @@ extern "C" {
  * dctq_forward_float / dctq_inverse to their lane-per-block kernels when 1. */
 int dctq_diag_plan_set_variant(dctq_plan *plan, int variant);
 
+/* Launch every kernel of a plan as if the device had num_cus CUs (1..4096; the
+ * grids are capped per CU), so a test-sized input gives each wave many batches
+ * (test-only: on the full grid a wave of the fused Huffman kernel sees about one
+ * batch of a 4K frame stack, so its row carry between batches runs only then). */
+int dctq_diag_plan_set_num_cus(dctq_plan *plan, int num_cus);
+
 /* Moves exactly the bytes dctq_forward_quant_planes moves (same grid, prefetch,
  * LDS stage and 1 KiB stores) with no arithmetic.  coef[k] receives pixel bytes,
  * NOT coefficients.  Its time is the memory ceiling of the forward kernel's own

@@ -94,6 +94,14 @@ int dctq_diag_plan_set_variant(dctq_plan *plan, int variant) {
     return DCTQ_OK;
 }
 
+int dctq_diag_plan_set_num_cus(dctq_plan *plan, int num_cus) {
+    DCTQ_ENTRY;
+    if (!plan) return dctq::fail(DCTQ_EINVAL, "plan is NULL");
+    if (num_cus < 1 || num_cus > 4096) return dctq::fail(DCTQ_EINVAL, "num_cus must be 1..4096");
+    plan->num_cus = num_cus;
+    return DCTQ_OK;
+}
+
 int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               void *stream) {
     DCTQ_ENTRY;

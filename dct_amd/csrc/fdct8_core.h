@@ -396,6 +396,54 @@ __device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c
     return (int)round(out / m);
 }
 
+// exact_from_rows_lds() for e <= 8 entries of one pass, 8 lanes per entry
+// (lane = 8 * entry + k): lane k pulls row k of the entry's block from the
+// owning lane and sums it in the reference's order (temp[k][j], src/dct.c:57-66);
+// the group's 8 row sums are broadcast to every lane of the group (ds_swizzle)
+// and summed in row order (src/dct.c:67-74); the group's first lane stores
+// round(out / M) (src/quantization.c:124).  ~100 VALU per lane against ~290 for
+// one entry per lane: for passes with few entries (the fused Huffman kernel,
+// where most batches hold one or two).  Non-adaptive plans only (the adaptive
+// divisor needs the whole block's variance).
+// out += D[i][q] * (row q's sum, from lane 8 * group + q: ds_swizzle with
+// and_mask 0x18, or_mask q), q = Q .. 7 in order.
+template <int Q>
+__device__ __forceinline__ void group8_sum(uint64_t tb, const double *di, double &out) {
+    if constexpr (Q < 8) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)tb, 0x18 | (Q << 5));
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(tb >> 32), 0x18 | (Q << 5));
+        out += di[Q] * __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        group8_sum<Q + 1>(tb, di, out);
+    }
+}
+
+__device__ __forceinline__ void exact_grouped8(const ExactTables *tab, const uint2 (&cur)[8], int16_t *st16,
+                                               const uint16_t *scr, int lane, uint32_t e) {
+    const int grp = lane >> 3, k = lane & 7;
+    const uint32_t ent = (uint32_t)grp < e ? (uint32_t)scr[grp] : 0u;
+    const int src = (int)(ent >> 6), c = (int)(ent & 63u);
+    uint32_t rx = 0, ry = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)cur[q].x);
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)cur[q].y);
+        rx = k == q ? x : rx;
+        ry = k == q ? y : ry;
+    }
+    const double *dj = tab->dct + (c & 7) * 8;  // D^T[l][j]
+    const double *di = tab->dct + (c >> 3) * 8;  // D[i][k]
+    double t = 0.0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const uint32_t w = l < 4 ? rx : ry;
+        t += ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
+    }
+    const uint64_t tb = __builtin_bit_cast(uint64_t, t);
+    double out = 0.0;
+    group8_sum<0>(tb, di, out);
+    if (k == 0 && (uint32_t)grp < e) st16[src * (kPitch2 / 2) + c] = (int16_t)(int)round(out / tab->quant[c]);
+}
+
 // Phase 1: the forward of one 64-block batch into the stage plus the constant-
 // block DC table; returns the lane's remaining tie flags (none for invalid lanes).
 template <bool ADAPTIVE, bool VAR>
@@ -416,7 +464,7 @@ __device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict_
 // value (tables in LDS) and writes it into the stage.  `scr` = 64 uint16 of the
 // wave's LDS (entry = coefficient | block lane << 6).  Call after the prefetch
 // fence.  Returns the entries this lane resolved.
-template <bool ADAPTIVE>
+template <bool ADAPTIVE, bool GROUP8 = false>
 __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab, const uint2 (&cur)[8], uint4 *stage,
                                                          uint16_t *scr, int lane, int wv, uint32_t &mlo,
                                                          uint32_t &mhi) {
@@ -436,6 +484,13 @@ __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab,
             has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
         }
         wave_sync();
+        if constexpr (GROUP8 && !ADAPTIVE) {
+            if (e <= 8u) {  // wave-uniform
+                exact_grouped8(tab, cur, st16, scr, lane, e);
+                wave_sync();
+                continue;
+            }
+        }
         const uint32_t ent = (uint32_t)lane < e ? (uint32_t)scr[lane] : 0u;
         const int src = (int)(ent >> 6);
         uint2 rows[8];  // the block's rows, from its owning lane (every lane takes part)

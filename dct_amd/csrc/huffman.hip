@@ -114,10 +114,43 @@ struct Hist {
 };
 
 // Occupancy of the lane's histogram: bit w-1 set while bucket w may hold nodes
-// (the merge jumps from one occupied bucket to the next).
-__device__ __forceinline__ void mark(uint64_t &occ, uint32_t w, uint32_t n) {
-    occ |= n ? 1ull << (w - 1) : 0ull;
-}
+// (the merge jumps from one occupied bucket to the next).  Occ64 is one uint64;
+// Occ32x2 two 32-bit halves, for the fused kernel: there the zero high half of
+// the first eight marks was a 64-bit constant it spilled (and the reload waited
+// for every load in flight, the next batch's rows included).  The standalone
+// kernel keeps Occ64 (the halves measured +2.6 % on extreme input there).
+struct Occ64 {
+    uint64_t m = 0;
+    __device__ __forceinline__ void first8(uint32_t w, uint32_t n) { m |= n ? 1ull << (w - 1) : 0ull; }
+    __device__ __forceinline__ bool any() const { return m != 0; }
+    __device__ __forceinline__ void set(uint32_t w) { m |= 1ull << (w - 1); }
+    __device__ __forceinline__ uint32_t pop() {
+        const uint32_t w = (uint32_t)__builtin_ctzll(m) + 1u;
+        m &= m - 1ull;
+        return w;
+    }
+};
+struct Occ32x2 {
+    uint32_t lo = 0, hi = 0;  // buckets 1..32, 33..64
+    __device__ __forceinline__ void first8(uint32_t w, uint32_t n) { lo |= n ? 1u << (w - 1) : 0u; }
+    __device__ __forceinline__ bool any() const { return (lo | hi) != 0; }
+    __device__ __forceinline__ void set(uint32_t w) {  // w in 1..64
+        if (w <= 32)
+            lo |= 1u << (w - 1);
+        else
+            hi |= 1u << (w - 33);
+    }
+    __device__ __forceinline__ uint32_t pop() {  // lowest occupied bucket, cleared
+        if (lo) {
+            const uint32_t w = (uint32_t)__builtin_ctz(lo) + 1u;
+            lo &= lo - 1u;
+            return w;
+        }
+        const uint32_t w = (uint32_t)__builtin_ctz(hi) + 33u;
+        hi &= hi - 1u;
+        return w;
+    }
+};
 
 constexpr uint32_t kSent = 0xFFFFFFFFu;  // a zero coefficient (dropped)
 
@@ -660,12 +693,12 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int la
     if (lane_merge) {
         // occupancy of the leaf buckets, read back up to the wave's largest leaf weight
         // (cheaper than marking every leaf; this wave's LDS atomics are already ordered)
-        uint64_t occ = 0;
+        std::conditional_t<FWD, Occ32x2, Occ64> occ;
 #pragma unroll
         for (uint32_t w = 1; w <= 8; ++w)  // independent reads, in flight together
-            occ |= h.peek(w) ? 1ull << (w - 1) : 0ull;
+            occ.first8(w, h.peek(w));
         for (uint32_t w = 9; __builtin_amdgcn_ballot_w64(w <= lmax); ++w)
-            occ |= h.peek(w) ? 1ull << (w - 1) : 0ull;
+            if (h.peek(w)) occ.set(w);
         // Each lane jumps to its own next occupied bucket (lowest bit of occ), so the
         // loop runs as many steps as the busiest lane has occupied buckets, not up to
         // its largest weight.  New weights (pending + w, 2w) are above w, so the scan
@@ -673,16 +706,15 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int la
         // The lane is done when no bucket is left: its last node (the root) is then
         // `pending`, and every bucket it held nodes in was taken (cleared).  The step
         // cap only bounds the loop.
-        for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ != 0); ++step) {
-            if (occ) {
-                const uint32_t w = (uint32_t)__builtin_ctzll(occ) + 1u;
-                occ &= occ - 1ull;  // bucket w is emptied by this step
+        for (int step = 0; step < 130 && __builtin_amdgcn_ballot_w64(occ.any()); ++step) {
+            if (occ.any()) {
+                const uint32_t w = occ.pop();  // bucket w is emptied by this step
                 uint32_t c = h.take(w);
                 if (pending && c) {
                     const uint32_t nw = pending + w;
                     wpl += nw;
                     h.add(nw, 1);
-                    mark(occ, nw, 1);
+                    occ.set(nw);
                     --c;
                     pending = 0;
                 }
@@ -690,7 +722,7 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int la
                 if (pairs) {
                     wpl += pairs * 2 * w;
                     h.add(2 * w, pairs);
-                    mark(occ, 2 * w, 1);
+                    occ.set(2 * w);
                 }
                 if (c & 1) pending = w;
             }
@@ -753,14 +785,8 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
     return sort_tile_bits<FWD>(mine, ctr, lane, wv, nb, cl, next_tile);
 }
 
-#ifndef DCTQ_HP_DIRECT
-#define DCTQ_HP_DIRECT 1  // the size path reads the rows where the forward left them; 0: copy them to the tile layout first (A/B: direct is -2.8 to -4.5 %)
-#endif
-#ifndef DCTQ_HP_PREFETCH
-#define DCTQ_HP_PREFETCH 0  // A/B: huffman_from_pixels prefetches the next batch's rows into registers
-#endif
-#if DCTQ_HP_PREFETCH && DCTQ_HP_DIRECT
-#error "DCTQ_HP_PREFETCH is only wired into the tile-layout path (DCTQ_HP_DIRECT=0): the direct path never refreshes the prefetched rows"
+#ifndef DCTQ_HP_GROUP8
+#define DCTQ_HP_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped8): -4.1 % uniform, -3.1 % smooth
 #endif
 #ifndef DCTQ_HUF_MIN_WAVES
 #define DCTQ_HUF_MIN_WAVES 3
@@ -824,11 +850,14 @@ hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bi
 // ============================================================================
 // The reference pipeline's per-block size straight from pixels (SURVEY 8(f)4 fed
 // by 8(a)): forward DCT + quantization (fdct8_core.h, ties resolved in place in
-// the reference's order) -> the tile in this kernel's layout -> tile_bits.  The
+// the reference's order) -> tile_bits on the rows where the forward left them
+// (copying them into the tile layout first was 2.8-4.5 % slower).  The
 // coefficients never leave LDS: 64 B read and 4 B written per block, against
 // 192 + 132 for dctq_forward_quant_planes followed by dctq_huffman_bits.
 // Same grid, occupancy (3 waves/SIMD) and LDS as huffman_bits_kernel, plus the
-// exact path's 1 KiB table copy.
+// exact path's 1 KiB table copy.  The next batch's rows are loaded into `cur`
+// as soon as the tie pass is done with them, so the loads fly through the size
+// computation (-3.4 %).
 template <bool ADAPTIVE>
 __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_pixels_kernel(EncodeSet es,
                                                                                               const DevTables *__restrict__ dev,
@@ -848,10 +877,8 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
     const PlaneSet &ps = es.ps;
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kHufWaves;
-#if DCTQ_HP_PREFETCH
-    uint2 nxt[8];
-    prefetch_batch(ps, blockIdx.x * kHufWaves + wv, lane, nxt);
-#endif
+    uint2 cur[8];
+    prefetch_batch(ps, blockIdx.x * kHufWaves + wv, lane, cur);
     for (uint32_t g = blockIdx.x * kHufWaves + wv; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];
@@ -859,13 +886,6 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         const uint32_t n = b * 64 + lane;
         const bool valid = n < (uint32_t)p.nblk;
         const int nb = (uint32_t)p.nblk - b * 64 < 64u ? (int)((uint32_t)p.nblk - b * 64) : 64;
-        uint2 cur[8];
-#if DCTQ_HP_PREFETCH
-#pragma unroll
-        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-#else
-        load_rows(p, n, cur);
-#endif
         // the rows are in, and the previous batch's bits store has left before
         // LDS reads land in VGPRs (the store-data hazard)
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -874,9 +894,13 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         fdct8_compute<ADAPTIVE, false>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
         flat_dc_fix(dev, cur, stage, lane, wv, mlo);
         if (!valid) mlo = mhi = 0;
-        if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0)) (void)resolve_ties_compact<ADAPTIVE>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
+#ifdef DCTQ_HP_ABLATE_TIES  // timing ablation only: flagged coefficients keep their fast-path value
+        mlo = mhi = 0;
+#endif
+        if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0))
+            (void)resolve_ties_compact<ADAPTIVE, DCTQ_HP_GROUP8>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
         wave_sync();
-#if DCTQ_HP_DIRECT
+        prefetch_batch(ps, g + step, lane, cur);  // the rows are dead now; nothing past the last batch
         if (nb < 64) {  // blocks past the end are empty
             if (lane >= nb) {
 #pragma unroll
@@ -886,30 +910,6 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
             wave_sync();
         }
         const uint32_t out = tile_bits<true>(mine, ctr, lane, wv, nb, [] {});
-#else
-        // the block's 128 B from the forward stage (pitch kPitch2, 8-B aligned) to
-        // this kernel's layout: piece q of block b at b * 128 + 16 * (q ^ ((b >> 1) & 7))
-        uint4 row[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const uint2 lo = *reinterpret_cast<const uint2 *>(mine + lane * kPitch2 + 16 * q);
-            const uint2 hi = *reinterpret_cast<const uint2 *>(mine + lane * kPitch2 + 16 * q + 8);
-            row[q] = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane's reads are done before any write
-        wave_sync();
-        const int sw = (lane >> 1) & 7;
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-            *reinterpret_cast<uint4 *>(mine + lane * 128 + 16 * (q ^ sw)) =
-                lane < nb ? row[q] : make_uint4(0, 0, 0, 0);  // blocks past the end are empty
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        wave_sync();
-#if DCTQ_HP_PREFETCH
-        prefetch_batch(ps, g + step, lane, nxt);  // in flight through the size computation
-#endif
-        const uint32_t out = tile_bits(mine, ctr, lane, wv, nb, [] {});
-#endif
         const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
             bits + es.blk_first[k] + (size_t)b * 64, (short)0, nb * 4, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
@@ -923,7 +923,7 @@ hipError_t launch_huffman_from_pixels(const EncodeSet &es, const DevTables *dev,
                                       hipStream_t stream, int num_cus) {
     const uint32_t nbatch = es.ps.first[es.ps.n];
     long long grid = ((long long)nbatch + kHufWaves - 1) / kHufWaves;
-    const long long cap = (long long)num_cus * DCTQ_HUF_GRID_PER_CU;
+    const long long cap = (long long)num_cus * DCTQ_HUF_GRID_PER_CU;  // a persistent grid (3 per CU) is +11 %
     if (grid > cap) grid = cap;
     if (grid < 1) return hipSuccess;
     if (adaptive)

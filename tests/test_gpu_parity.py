@@ -1145,13 +1145,33 @@ def test_huffman_bits_planes_from_pixels(T, dm):
     want = O.huffman_bits_plane(O.forward_plane(px, 50, 0))
     got = dm.Plan(50, 0).huffman_bits_planes([gpu_px(T, px)]).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, want)
-    # a 4K 4:2:0 stack (many batches per wave on the 16-per-CU grid)
+    # a 4K 4:2:0 stack
     plan = dm.Plan(50, 0)
     planes = [dm.synth(3, "uniform", 3840, 2160, 4), dm.synth(4, "uniform", 1920, 1080, 8)]
     want = dm.huffman_bits(T.cat(plan.forward_quant_planes(planes)))
     got = plan.huffman_bits_planes(planes)
     T.cuda.synchronize()
     assert T.equal(got, want)
+
+
+def test_huffman_bits_planes_many_batches_per_wave(T, dm):
+    """The fused kernel carries each next batch's rows in registers from one iteration to
+    the next (loaded as soon as the tie pass is done with the current ones).  On the full
+    grid a wave sees about one batch, so the plans here launch as if the device had 1-3
+    CUs (dctq_diag_plan_set_num_cus): ~16-50 batches per wave, plane changes inside a
+    wave's sequence, ragged planes with partial last batches, tie-heavy and adaptive plans.
+    Reference: the two launches (forward_quant_planes -> huffman_bits), bit-exact."""
+    rng = np.random.default_rng(12)
+    for kind, q, ad, cus in [("uniform", 50, 0, 1), ("uniform", 50, 1, 2), ("extreme", 10, 0, 1),
+                             ("smooth", 90, 0, 3), ("uniform", 100, 0, 1), ("extreme", 50, 1, 1)]:
+        planes = [dm.synth(int(rng.integers(1 << 30)), kind, 3840, 2160),
+                  dm.synth(int(rng.integers(1 << 30)), kind, 8 * 123, 8 * 67, 3),
+                  dm.synth(int(rng.integers(1 << 30)), kind, 8 * 31, 8 * 7)]
+        want = dm.huffman_bits(T.cat(dm.Plan(q, ad).forward_quant_planes(planes)))
+        got = dm.Plan(q, ad, num_cus=cus).huffman_bits_planes(planes)
+        T.cuda.synchronize()
+        bad = (got != want).nonzero()
+        assert bad.numel() == 0, (kind, q, ad, cus, bad[:8].flatten().tolist())
 
 
 def test_encode_planes_fused(T, dm):

