@@ -464,6 +464,9 @@ __device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict_
 // value (tables in LDS) and writes it into the stage.  `scr` = 64 uint16 of the
 // wave's LDS (entry = coefficient | block lane << 6).  Call after the prefetch
 // fence.  Returns the entries this lane resolved.
+#ifndef DCTQ_GROUP8_MAX
+#define DCTQ_GROUP8_MAX 8u  // GROUP8 passes with up to this many entries run in rounds of 8 lanes per entry
+#endif
 template <bool ADAPTIVE, bool GROUP8 = false>
 __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab, const uint2 (&cur)[8], uint4 *stage,
                                                          uint16_t *scr, int lane, int wv, uint32_t &mlo,
@@ -485,8 +488,9 @@ __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab,
         }
         wave_sync();
         if constexpr (GROUP8 && !ADAPTIVE) {
-            if (e <= 8u) {  // wave-uniform
-                exact_grouped8(tab, cur, st16, scr, lane, e);
+            if (e <= DCTQ_GROUP8_MAX) {  // wave-uniform: rounds of 8 entries (~100 VALU each, against ~290 for a pass)
+                for (uint32_t e0 = 0; e0 < e; e0 += 8u)
+                    exact_grouped8(tab, cur, st16, scr + e0, lane, e - e0 < 8u ? e - e0 : 8u);
                 wave_sync();
                 continue;
             }

@@ -4,7 +4,7 @@ with var_num, then dctq_inverse per plane) on the bench workload: F 4K 4:2:0 fra
 (Y planes + Cb/Cr planes, two planes per launch).  Also times diagnostic builds
 tools/ubench/libvar_*.so (tools/ubench/variant.sh) of the fused kernel, interleaved.
 
-    python tools/rt_bench.py [F] [--adaptive]
+    python tools/rt_bench.py [F] [--adaptive] [--kind=uniform] [--q=50]
 """
 import ctypes as C
 import glob
@@ -21,9 +21,11 @@ import dct_amd  # noqa: E402
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 F = int(args[0]) if args else 64
 AD = int("--adaptive" in sys.argv)
+KIND = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--kind=")), "uniform")
+Q = int(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--q=")), "50"))
 ROUNDS = 10
-luma = dct_amd.synth(7, "uniform", 3840, 2160, F)
-chroma = dct_amd.synth(8, "uniform", 1920, 1080, 2 * F)
+luma = dct_amd.synth(7, KIND, 3840, 2160, F)
+chroma = dct_amd.synth(8, KIND, 1920, 1080, 2 * F)
 planes = [luma, chroma]
 nbs = [F * 480 * 270, 2 * F * 240 * 135]
 nblk = sum(nbs)
@@ -49,9 +51,9 @@ for name, path in libs.items():
     L.dctq_plan_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.dctq_round_trip_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int] + [C.c_void_p] * 4
     h = C.c_void_p()
-    assert L.dctq_plan_create(50, AD, C.byref(h)) == 0
+    assert L.dctq_plan_create(Q, AD, C.byref(h)) == 0
     runs[name] = (lambda L=L, h=h: L.dctq_round_trip_planes(h, descs, 2, arr(coef2), None, arr(rec2), stream))
-plan = dct_amd.Plan(50, AD)
+plan = dct_amd.Plan(Q, AD)
 
 
 def unfused():
@@ -80,7 +82,7 @@ for r in range(ROUNDS + 2):
 for name, ts in times.items():
     med = statistics.median(ts)
     bpb = 584 if name == "unfused" else 448
-    print(f"{name:22s} adaptive={AD} median {med*1e6:8.1f} us  {nblk/med/1e9:6.2f} G blocks/s  "
+    print(f"{name:22s} {KIND} q{Q} adaptive={AD} median {med*1e6:8.1f} us  {nblk/med/1e9:6.2f} G blocks/s  "
           f"{nblk*bpb/med/1e9:6.0f} GB/s ({bpb} B/block)")
 # correctness of the default library against the unfused pair (after all rounds)
 runs["fused"]()
