@@ -967,7 +967,9 @@ def main():
                        "world_size": world, "backend": dist.get_backend() if dist_on else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
-                         "kernel": f"fdct8_quant_v2<{bool(args.adaptive)}, false, false>".lower(),
+                         "kernel": dct_amd.forward_kernel(args.quality, args.adaptive,
+                                                          -(-nblk_y // 64) + -(-nblk_c // 64),
+                                                          torch.cuda.get_device_properties(dev).multi_processor_count),
                          "avg_launch_us": avg_launch_s * 1e6, "launches_per_step": launches,
                          "bytes_per_launch": avg_launch_bytes, "movement_ceiling": movement},
             "cpu_baseline": cpu,

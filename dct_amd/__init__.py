@@ -68,6 +68,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
             "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
             "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
             "dctq_debug_dc_table": ([i, vp], i),
+            "dctq_debug_forward_kernel": ([i, i, ll, i], i),
         })
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -396,6 +397,13 @@ def synth(seed: int, kind, width: int, height: int, nframes: int = 1, device="cu
     d = plane_desc(out)
     _check(lib().dctq_synth(C.c_uint64(seed), k, C.byref(d), _stream_ptr(stream)))
     return out
+
+
+def forward_kernel(quality: int, adaptive: bool, batches: int, num_cus: int) -> str:
+    """Name of the forward kernel dctq_forward_quant_planes launches for this plan over
+    `batches` 64-block batches on num_cus CUs (host-only, dctq_debug_forward_kernel)."""
+    v = diag().dctq_debug_forward_kernel(int(quality), int(bool(adaptive)), int(batches), int(num_cus))
+    return f"fdct8_quant_v{v}<{str(bool(adaptive)).lower()}, false, false>"
 
 
 def debug_tables(quality: int, adaptive: bool = False):

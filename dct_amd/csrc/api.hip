@@ -326,7 +326,8 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
     {
         std::lock_guard<std::mutex> stash_guard(g_stash_mu);
         e = dctq::launch_fdct8_quant(ps, plan->fast, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
-                                     plan->variant, plan->num_cus, dctq::RingSource{stash_for, &sc});
+                                     plan->variant, plan->num_cus, dctq::RingSource{stash_for, &sc},
+                                     plan->host.quant[0] <= 1.0);  // the same test as dctq_debug_forward_kernel
     }
     if (sc.err == hipErrorStreamCaptureUnsupported)
         return fail(DCTQ_EINVAL, "the tie-path stash of this stream is smaller than this launch needs: run the launch "

@@ -52,6 +52,10 @@ int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
 
 /* Host-only introspection for the CPU tests (no GPU needed). */
+/* The forward kernel (1, 2, 3 = fdct8_quant_v1/v2/v3) dctq_forward_quant_planes runs
+ * for a plan of this quality / adaptive mode over `batches` 64-block batches on a
+ * device of num_cus CUs (bench.py names the kernel its roofline is measured on). */
+int dctq_debug_forward_kernel(int quality, int adaptive, long long batches, int num_cus);
 int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *dct, double *quant);
 int dctq_debug_dc_table(int quality, int16_t *out);
 int dctq_debug_fastdiv(uint32_t d, uint32_t n);

@@ -125,9 +125,13 @@ struct RingSource {
     void *(*get)(void *ctx, size_t bytes);
     void *ctx;
 };
+// tie_heavy: the plan's DC divisor is 1 (q >= 97): the rational coefficients tie in
+// ~1 block of 8, and the product dispatch keeps the queue kernel (v2) for it.
 hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
                               unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus,
-                              const RingSource &ring);
+                              const RingSource &ring, bool tie_heavy);
+// the forward kernel (1, 2 or 3 = fdct8_quant_v1/v2/v3) launch_fdct8_quant runs
+int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy);
 // bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
 size_t fdct8_ring_bytes(int workgroups);
 // diagnostic: fdct8_quant_v2's data movement without arithmetic (fdct8.hip)

@@ -173,6 +173,14 @@ int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *d
     return DCTQ_OK;
 }
 
+int dctq_debug_forward_kernel(int quality, int adaptive, long long batches, int num_cus) {
+    (void)adaptive;
+    double q[64];
+    dctq_host::quant_matrix(8, dctq_host::clamp_quality(quality), q);
+    const uint32_t nb = batches < 0 ? 0u : batches > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)batches;
+    return dctq::forward_kernel_for(2, nb, num_cus, q[0] <= 1.0);
+}
+
 int dctq_debug_dc_table(int quality, int16_t *out) {
     double d[64], q[64];
     dctq_host::dct_matrix(8, d);

@@ -268,6 +268,9 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
 #ifndef DCTQ_LAST_INPLACE
 #define DCTQ_LAST_INPLACE 1  // a wave's last batch empties the queue before its stores and resolves in place
 #endif
+#ifndef DCTQ_V2_GROUP8
+#define DCTQ_V2_GROUP8 0  // A/B: in-stage passes of <= 8 entries run 8 lanes per entry (exact_grouped8)
+#endif
 #ifndef DCTQ_INSTAGE_LANES
 // A batch with at least this many flagged blocks resolves its ties in the stage,
 // before its stores (resolve_in_stage); sparser batches queue them.  65 = never.
@@ -329,7 +332,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     if ((DCTQ_INSTAGE_LANES <= 64 && nflag >= DCTQ_INSTAGE_LANES) || (last && nflag > 0))
     {
         // tie-heavy batch: resolved in the stage before its stores (no stash, no patches)
-        const uint32_t n = resolve_ties_compact<ADAPTIVE>(tab, cur, stage, qc + qn, lane, wv, mlo, mhi);
+        const uint32_t n = resolve_ties_compact<ADAPTIVE, DCTQ_V2_GROUP8>(tab, cur, stage, qc + qn, lane, wv, mlo, mhi);
         if (STATS && n) atomicAdd(fallbacks, (unsigned long long)n);
     }
 
@@ -500,6 +503,12 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 // in ~78 % of batches), but when every wave has at most one batch (a single frame:
 // 512x512 = 64 batches, 4K = 2 025) v2's end-of-kernel drain -- vmcnt(0), stash
 // loads, fp64, patch stores -- is the whole tail of the launch.
+#ifndef DCTQ_V3_GROUP8
+#define DCTQ_V3_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped8)
+#endif
+#ifndef DCTQ_FWD_INPLACE
+#define DCTQ_FWD_INPLACE 1  // the product dispatch picks v3 (in-place ties) at every size unless the plan is tie-heavy
+#endif
 template <bool ADAPTIVE, bool VAR, bool STATS>
 __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, const DevTables *__restrict__ dev,
                                                               unsigned long long *fallbacks) {
@@ -531,7 +540,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         // the prefetch wait (retires the previous batch's stores too), then LDS reads
         asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                      "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-        resolved += resolve_ties_compact<ADAPTIVE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+        resolved += resolve_ties_compact<ADAPTIVE, DCTQ_V3_GROUP8>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         wave_sync();
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
@@ -565,15 +574,23 @@ size_t fdct8_ring_bytes(int workgroups) { return (size_t)workgroups * kFWaves * 
 
 hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
                               unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus,
-                              const RingSource &ring) {
+                              const RingSource &ring, bool tie_heavy) {
     const bool a = adaptive != 0, v = ps.var[0] != nullptr, s = fallbacks != nullptr;
-    if (variant == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
-    // at most one batch per wave of the resident grid (16 waves per CU: 4 per SIMD,
-    // VGPR-bound): in-place ties, no stash and no drain tail
-    const bool single = ps.first[ps.n] <= (uint32_t)(num_cus * 16);
-    if (variant == 3 || (variant == 2 && single))  // variant 4: the queue kernel at any size (A/B)
-        DCTQ_SELECT(return launch_v3, a, v, s, (ps, dev, fallbacks, stream, num_cus));
+    const int kern = forward_kernel_for(variant, ps.first[ps.n], num_cus, tie_heavy);
+    if (kern == 1) DCTQ_SELECT(return launch_v1, a, v, s, (ps, t, dev, fallbacks, stream));
+    if (kern == 3) DCTQ_SELECT(return launch_v3, a, v, s, (ps, dev, fallbacks, stream, num_cus));
     DCTQ_SELECT(return launch_v2, a, v, s, (ps, t, dev, fallbacks, stream, num_cus, ring));
+}
+
+int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy) {
+    if (variant == 1) return 1;
+    if (variant == 3) return 3;
+    if (variant == 4) return 2;  // the queue kernel at any size (A/B)
+    // in-place ties (v3) unless the plan is tie-heavy; and always when every wave of
+    // the resident grid (16 waves per CU: 4 per SIMD, VGPR-bound) has at most one
+    // batch, where v2's end-of-kernel drain would be the whole tail
+    const bool single = nbatch <= (uint32_t)(num_cus * 16);
+    return single || (DCTQ_FWD_INPLACE && !tie_heavy) ? 3 : 2;
 }
 
 // ============================================================================

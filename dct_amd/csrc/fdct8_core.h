@@ -401,10 +401,10 @@ __device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c
 // owning lane and sums it in the reference's order (temp[k][j], src/dct.c:57-66);
 // the group's 8 row sums are broadcast to every lane of the group (ds_swizzle)
 // and summed in row order (src/dct.c:67-74); the group's first lane stores
-// round(out / M) (src/quantization.c:124).  ~100 VALU per lane against ~290 for
+// round(out / M) (src/quantization.c:124) and returns 1 (its entry resolved).  ~100 VALU per lane against ~290 for
 // one entry per lane: for passes with few entries (the fused Huffman kernel,
-// where most batches hold one or two).  Non-adaptive plans only (the adaptive
-// divisor needs the whole block's variance).
+// where most batches hold one or two).  Adaptive plans sum the block's variance
+// terms over the group (group8_add).
 // out += D[i][q] * (row q's sum, from lane 8 * group + q: ds_swizzle with
 // and_mask 0x18, or_mask q), q = Q .. 7 in order.
 template <int Q>
@@ -417,8 +417,17 @@ __device__ __forceinline__ void group8_sum(uint64_t tb, const double *di, double
     }
 }
 
-__device__ __forceinline__ void exact_grouped8(const ExactTables *tab, const uint2 (&cur)[8], int16_t *st16,
-                                               const uint16_t *scr, int lane, uint32_t e) {
+// Sum of v over the lane's group of 8 (ds_swizzle xor 1, 2, 4 within 32 lanes).
+__device__ __forceinline__ uint32_t group8_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (1 << 10));
+    v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (2 << 10));
+    v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (4 << 10));
+    return v;
+}
+
+template <bool ADAPTIVE>
+__device__ __forceinline__ uint32_t exact_grouped8(const ExactTables *tab, const uint2 (&cur)[8], int16_t *st16,
+                                                   const uint16_t *scr, int lane, uint32_t e) {
     const int grp = lane >> 3, k = lane & 7;
     const uint32_t ent = (uint32_t)grp < e ? (uint32_t)scr[grp] : 0u;
     const int src = (int)(ent >> 6), c = (int)(ent & 63u);
@@ -441,7 +450,22 @@ __device__ __forceinline__ void exact_grouped8(const ExactTables *tab, const uin
     const uint64_t tb = __builtin_bit_cast(uint64_t, t);
     double out = 0.0;
     group8_sum<0>(tb, di, out);
-    if (k == 0 && (uint32_t)grp < e) st16[src * (kPitch2 / 2) + c] = (int16_t)(int)round(out / tab->quant[c]);
+    double m = tab->quant[c];
+    if (ADAPTIVE) {  // the block's exact variance from the group's rows (exact_from_rows_lds)
+        const uint32_t s1 = group8_add(__builtin_amdgcn_udot4(ry, 0x01010101u, __builtin_amdgcn_udot4(rx, 0x01010101u, 0u, false), false));
+        const uint32_t s2 = group8_add(__builtin_amdgcn_udot4(ry, ry, __builtin_amdgcn_udot4(rx, rx, 0u, false), false));
+        if (c != 0) {
+            const int32_t sx = (int32_t)s1 - 8192;
+            const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
+            m = m * adaptive_scale(64 * sxx - sx * sx);
+            if (m < 1.0) m = 1.0;
+        }
+    }
+    if (k == 0 && (uint32_t)grp < e) {
+        st16[src * (kPitch2 / 2) + c] = (int16_t)(int)round(out / m);
+        return 1u;
+    }
+    return 0u;
 }
 
 // Phase 1: the forward of one 64-block batch into the stage plus the constant-
@@ -487,10 +511,10 @@ __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab,
             has = __builtin_amdgcn_ballot_w64((mlo | mhi) != 0);
         }
         wave_sync();
-        if constexpr (GROUP8 && !ADAPTIVE) {
+        if constexpr (GROUP8) {
             if (e <= DCTQ_GROUP8_MAX) {  // wave-uniform: rounds of 8 entries (~100 VALU each, against ~290 for a pass)
                 for (uint32_t e0 = 0; e0 < e; e0 += 8u)
-                    exact_grouped8(tab, cur, st16, scr + e0, lane, e - e0 < 8u ? e - e0 : 8u);
+                    mine += exact_grouped8<ADAPTIVE>(tab, cur, st16, scr + e0, lane, e - e0 < 8u ? e - e0 : 8u);
                 wave_sync();
                 continue;
             }

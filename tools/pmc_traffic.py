@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--kind", required=True)
     ap.add_argument("--quality", type=int, default=50)
     ap.add_argument("--adaptive", type=int, default=0)
-    ap.add_argument("--kernel", default="fdct8_quant_v2")
+    ap.add_argument("--kernel", default="fdct8_quant_v")  # v2 or v3, whichever the dispatch ran
     ap.add_argument("--launches", type=int, default=1, help="forward-quant dispatches per bench step")
     ap.add_argument("-o", "--out", default="profiles/traffic.json")
     a = ap.parse_args()
