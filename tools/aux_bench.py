@@ -1,5 +1,8 @@
 """Time the non-quantizing kernels (forward_float, inverse) on 64 x 4K luma
-planes, interleaved, HIP events per launch; report % of 8 TB/s on algorithmic bytes."""
+planes, interleaved, HIP events per launch; report % of 8 TB/s on algorithmic bytes.
+Labels: v1 = plan variant 1 (the one-workgroup-per-256-blocks kernels), v2 = plan
+variant 2 (the product dispatch: paired lane-per-block kernels; the forward with
+var_num runs whichever quantizing kernel the dispatch picks, fdct8_quant_v3 at q50)."""
 import os
 import statistics
 import sys
