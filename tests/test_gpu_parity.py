@@ -252,11 +252,12 @@ def test_forced_kernels_adversarial_and_counter(T, dm, variant):
 
 
 def test_mid_size_tie_heavy_stream(T, dm):
-    """More than 4096 64-block batches (the product dispatch then runs the v2 queue
-    kernel, not v3) of tie-heavy content: step blocks (a quarter of the DCs are
-    exact ties), 0/255 extremes and a plane whose batches alternate between step
-    blocks and uniform noise (both of v2's tie paths in one launch), several
-    qualities, both modes."""
+    """More than 4096 64-block batches of tie-heavy content: step blocks (a quarter
+    of the DCs are exact ties), 0/255 extremes and a plane whose batches alternate
+    between step blocks and uniform noise, several qualities, both modes.  Through
+    the product dispatch (v3, in-place grouped passes, for every plan with DC divisor
+    > 1; v2 at q100) and with the v2 queue kernel forced (variant 4: both of its tie
+    paths, the stage and the queue, in one launch)."""
     import oracle as O
     rng = np.random.default_rng(31)
     step = _step_blocks(rng, 270, 1024)  # 276 480 blocks = 4320 batches
@@ -269,14 +270,19 @@ def test_mid_size_tie_heavy_stream(T, dm):
     for px in (step, ext, mixed):
         g = gpu_px(T, px)
         for q, ad in [(50, 0), (10, 1), (90, 0), (100, 1)]:
-            plan = dm.Plan(q, ad)
-            cnt = T.zeros(1, dtype=T.int64, device="cuda")
-            plan.set_fallback_counter(cnt)
-            got = plan.forward_quant(g).cpu().numpy()
-            plan.set_fallback_counter(None)
-            assert np.array_equal(got, O.forward_plane(px, q, ad, 16)), (q, ad)
+            want = O.forward_plane(px, q, ad, 16)
+            counts = []
+            for variant in (None, 4):
+                plan = dm.Plan(q, ad, variant=variant)
+                cnt = T.zeros(1, dtype=T.int64, device="cuda")
+                plan.set_fallback_counter(cnt)
+                got = plan.forward_quant(g).cpu().numpy()
+                plan.set_fallback_counter(None)
+                assert np.array_equal(got, want), (q, ad, variant)
+                counts.append(int(cnt.item()))
+            assert counts[0] == counts[1], (q, ad, counts)  # every flagged coefficient, either kernel
             if q == 50 and px is step:
-                assert int(cnt.item()) > 1000
+                assert counts[0] > 1000
 
 
 def test_plans_cheap_and_stash_per_stream(T, dm):
@@ -287,7 +293,8 @@ def test_plans_cheap_and_stash_per_stream(T, dm):
     stash (<= 256 MiB); the same plan on two streams at once (each stream its
     own stash) gives the oracle's coefficients on both."""
     import oracle as O
-    px = dm.synth(4242, "uniform", 3840, 2160, 3)  # 388 800 blocks: > 16 waves x 256 CUs of batches -> v2 queue
+    # 388 800 blocks: > 16 waves x 256 CUs of batches, so tie-heavy plans (q >= 97) run the v2 queue kernel
+    px = dm.synth(4242, "uniform", 3840, 2160, 3)
     outs = [T.empty((3 * 480 * 270, 64), dtype=T.int16, device="cuda") for _ in range(2)]
     T.cuda.synchronize()
     free0 = T.cuda.mem_get_info()[0]
@@ -296,19 +303,19 @@ def test_plans_cheap_and_stash_per_stream(T, dm):
     free1 = T.cuda.mem_get_info()[0]
     assert free0 - free1 < (1 << 30), (free0 - free1) / 2 ** 20
     side = T.cuda.Stream()
-    for p in plans[::10]:
+    for p in plans[::10] + plans[96:]:  # v3 (no stash) and q97..q100 (v2: the stash)
         p.forward_quant(px, out=outs[0])
     T.cuda.synchronize()
     free2 = T.cuda.mem_get_info()[0]
     assert free1 - free2 <= (256 << 20) + (16 << 20), (free1 - free2) / 2 ** 20
-    p = plans[50]  # q51, adaptive
+    p = plans[98]  # q99, adaptive: v2
     side.wait_stream(T.cuda.current_stream())
     p.forward_quant(px, out=outs[0])
     with T.cuda.stream(side):
         p.forward_quant(px, out=outs[1], stream=side)
     T.cuda.synchronize()
     host = px.cpu().numpy()
-    want = np.concatenate([O.forward_plane(host[f], 51, 1, 8) for f in range(3)])
+    want = np.concatenate([O.forward_plane(host[f], 99, 1, 8) for f in range(3)])
     assert np.array_equal(outs[0].cpu().numpy(), want)
     assert np.array_equal(outs[1].cpu().numpy(), want)
 
