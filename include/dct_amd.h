@@ -44,8 +44,9 @@ typedef struct dctq_plan dctq_plan;
  * A plan holds only its ~4 KB of tables in device memory; it is reusable and
  * cheap to keep (one per quality is fine).  The forward kernel's tie-path stash
  * is the library's, one per (device, stream): allocated by the first forward
- * launch on a stream that needs it (a launch with more 64-block batches than
- * the device has resident waves), sized to that launch's grid (8 KiB per wave,
+ * launch on a stream that needs it (a tie-heavy plan, q >= 97, over more 64-block
+ * batches than the device has resident waves; other plans resolve their ties in
+ * place), sized to that launch's grid (8 KiB per wave,
  * at most 256 MiB on a 256-CU MI355X) and kept for later launches on the same
  * stream.  Under hipGraph capture, run the launch once on the stream first. */
 int dctq_plan_create(int quality, int adaptive, dctq_plan **plan);
