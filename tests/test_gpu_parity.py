@@ -446,6 +446,61 @@ def _step_blocks(rng, by, bx):
     return np.ascontiguousarray(blk.transpose(0, 2, 1, 3).reshape(by * 8, bx * 8))
 
 
+def _tie_count_plane(rng, counts):
+    """One 64-block batch per block row: row r holds counts[r] two-level step blocks whose
+    DC is an exact rounding tie at q50 (a != b, a + b = 2 mod 4: one exact-path entry
+    each), the rest constant blocks (their DC ties go to the constant-block table, not
+    the exact path).  So batch r's tie pass has exactly counts[r] entries."""
+    px = np.empty((8 * len(counts), 8 * 64), np.uint8)
+    for r, n in enumerate(counts):
+        vals = rng.integers(0, 256, 64)
+        pos = set(rng.choice(64, n, replace=False).tolist())
+        for b in range(64):
+            blk = np.full((8, 8), vals[b], np.uint8)
+            if b in pos:
+                while True:
+                    a, c = rng.integers(0, 256, 2)
+                    if a != c and (int(a) + int(c)) % 4 == 2:
+                        break
+                blk[:, :4], blk[:, 4:] = a, c
+            px[8 * r:8 * r + 8, 8 * b:8 * b + 8] = blk
+    return px
+
+
+def test_grouped_tie_passes(T, dm):
+    """Tie passes of 0..12 entries per batch around the grouped path's bound (<= 8
+    entries: 8 lanes per entry, exact_grouped8; above: one entry per lane) in every
+    kernel that resolves ties in place -- the forward (v3; v2 forced beside it), the
+    fused round trip, the encoder and the fused Huffman sizes -- for both modes, with
+    the fallback counter counting every entry once."""
+    import oracle as O
+    rng = np.random.default_rng(77)
+    counts = [0, 1, 2, 3, 5, 7, 8, 9, 12, 8, 1, 16] * 2
+    px = _tie_count_plane(rng, counts)
+    g = gpu_px(T, px)
+    for ad in (0, 1):
+        want = O.forward_plane(px, 50, ad)
+        got = {}
+        for variant in (None, 4):
+            plan = dm.Plan(50, ad, variant=variant)
+            cnt = T.zeros(1, dtype=T.int64, device="cuda")
+            plan.set_fallback_counter(cnt)
+            got[variant] = plan.forward_quant(g).cpu().numpy()
+            plan.set_fallback_counter(None)
+            assert np.array_equal(got[variant], want), (ad, variant)
+            assert int(cnt.item()) >= sum(counts), (ad, variant, int(cnt.item()))
+        plan = dm.Plan(50, ad)
+        coefs, recons = plan.round_trip_planes([g])
+        assert np.array_equal(T.cat(coefs).cpu().numpy(), want), ad
+        ec, off, sym = plan.encode_planes([g])
+        assert np.array_equal(T.cat(ec).cpu().numpy(), want), ad
+        woff, wsym = O.rle_encode_plane(want)
+        assert np.array_equal(off.cpu().numpy().view(np.uint32), woff), ad
+        assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), ad
+        bits = plan.huffman_bits_planes([g]).cpu().numpy().view(np.uint32)
+        assert np.array_equal(bits, O.huffman_bits_plane(want)), ad
+
+
 def test_forward_quant_planes(T, dm):
     """One launch over up to 4 planes of different geometry (ragged block counts, a
     multi-frame stack, a single block) equals per-plane calls and the oracle,
