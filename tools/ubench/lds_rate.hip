@@ -7,6 +7,8 @@
 #include <stdio.h>
 
 constexpr int kRows = 64, kIters = 4096;
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 template <int OP>
 __global__ __launch_bounds__(256) void lds_op(unsigned *out, unsigned long long *clk) {
@@ -30,8 +32,23 @@ __global__ __launch_bounds__(256) void lds_op(unsigned *out, unsigned long long 
                 acc ^= x;
             }
             if (OP == 4) acc += __hip_atomic_fetch_add(p, inc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            // 8- and 16-byte ops: lane l -> bytes 8l / 16l of a 512 / 1024-B row (conflict-free)
+            const unsigned a8 = (unsigned)(((r * 4 + (i & 3)) & 15) * 1024 + lane * 8);
+            const unsigned a16 = (unsigned)(((r * 4 + (i & 3)) & 15) * 1024 + lane * 16);
+            if (OP == 5) asm volatile("ds_write_b64 %0, %1" ::"v"(a8), "v"(v2u{acc, (unsigned)r}) : "memory");
+            if (OP == 6) asm volatile("ds_write_b128 %0, %1" ::"v"(a16), "v"(v4u{acc, (unsigned)r, acc, (unsigned)r}) : "memory");
+            if (OP == 7) {
+                v2u x;
+                asm volatile("ds_read_b64 %0, %1" : "=v"(x) : "v"(a8) : "memory");
+                acc ^= x[0];
+            }
+            if (OP == 8) {
+                v4u x;
+                asm volatile("ds_read_b128 %0, %1" : "=v"(x) : "v"(a16) : "memory");
+                acc ^= x[0];
+            }
         }
-        if (OP == 3) __builtin_amdgcn_s_waitcnt(0xC07F);  // the asm reads' results (acc ^= x above is not ordered)
+        if (OP == 3 || OP >= 7) __builtin_amdgcn_s_waitcnt(0xC07F);  // the asm reads' results (acc ^= x above is not ordered)
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -73,5 +90,9 @@ int main() {
     run<2>("ds_write_b32", cus);
     run<3>("ds_read_b32", cus);
     run<4>("ds_add_rtn_u32", cus);
+    run<5>("ds_write_b64", cus);
+    run<6>("ds_write_b128", cus);
+    run<7>("ds_read_b64", cus);
+    run<8>("ds_read_b128", cus);
     return 0;
 }
