@@ -100,7 +100,7 @@ constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) con
 #define DCTQ_STASH_DEDUP 1  // one pixel stash per flagged block and batch (its entries share it)
 #endif
 #ifndef DCTQ_ABLATE
-#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores, 2048 no final drain, 4096 drains compute but do not patch
+#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores, 2048 no final drain, 4096 drains compute but do not patch, 8192 in-stage passes without the fp64 evaluation
 #endif
 
 template <int K>
@@ -529,7 +529,10 @@ __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab,
         }
         if ((uint32_t)lane < e) {
             const int c = (int)(ent & 63u);
-            st16[src * (kPitch2 / 2) + c] = (int16_t)exact_from_rows_lds<ADAPTIVE>(rows, c, tab);
+            if (DCTQ_ABLATE & 8192)  // diagnostic: entries compacted and rows pulled, no fp64 evaluation
+                st16[src * (kPitch2 / 2) + c] = (int16_t)(rows[0].x ^ rows[3].y ^ rows[7].x ^ (uint32_t)c);
+            else
+                st16[src * (kPitch2 / 2) + c] = (int16_t)exact_from_rows_lds<ADAPTIVE>(rows, c, tab);
             ++mine;
         }
         wave_sync();  // the next pass rewrites scr
