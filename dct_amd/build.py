@@ -112,7 +112,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = {src: os.path.join(objdir, os.path.splitext(src)[0] + ".o") for src in srcs}
 
     def compile_one(src):
-        cmd = _flags() + ["-c", os.path.join(CSRC, src), "-o", objs[src]]
+        # a compilation-unit id from the file name, not hipcc's default hash of the
+        # path: the same sources give the same library bytes in any checkout
+        cuid = "dctamd_" + os.path.splitext(src)[0]
+        cmd = _flags() + [f"-cuid={cuid}", "-c", os.path.join(CSRC, src), "-o", objs[src]]
         if verbose:
             print(" ".join(cmd))
         return subprocess.run(cmd, capture_output=True, text=True)
