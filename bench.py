@@ -349,10 +349,6 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
         outs.append(torch.empty((rows * bw, 64), dtype=torch.int16, device=dev))
         counts.append([(hi - lo) * bw for lo, hi in (shard.split(p.shape[-2] // 8, world, r) for r in range(world))])
 
-    def once():
-        plan.forward_quant_planes(bands, outs=outs)
-        return shard.gather_planes(outs, counts)  # the three planes in one collective
-
     def timed(fn):
         r = fn()
         torch.cuda.synchronize()
@@ -364,18 +360,35 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
         torch.cuda.synchronize()
         return shard.max_over_ranks(time.perf_counter() - t0, dev), r
 
-    el, full = timed(once)
-    el_g, _ = timed(lambda: shard.gather_planes(outs, counts))  # the exchange alone
     want = plan.forward_quant_planes(planes)
-    ok = all(bool(torch.equal(f, w)) for f, w in zip(full, want))
     nblk = sum(w.shape[0] for w in want)
-    be = "RCCL all_gather_into_tensor" if dist.get_backend() == "nccl" else f"{dist.get_backend()} all_gather"
     rank = dist.get_rank()
     recv = sum(sum(c) - c[rank] for c in counts) * 128
-    return {"op": f"one 4K 4:2:0 frame in block-row bands over {world} ranks: forward_quant_planes(bands) + {be} "
-                  "of the Y/Cb/Cr coefficient planes", "frames": reps, "us_per_frame": el / reps * 1e6,
-            "blocks_per_s": nblk * reps / el, "gathered_equals_unsharded": ok,
-            "xgmi": shard.xgmi_report(recv, el_g / reps, world)}
+    by = {}
+    for m in shard.GATHER_METHODS:  # SURVEY 8(e)'s two shapes: the all-gather collective, direct peer pushes
+        def once():
+            plan.forward_quant_planes(bands, outs=outs)
+            return shard.gather_planes(outs, counts, method=m)  # the three planes in one collective / one group
+        el, full = timed(once)
+        el_g, _ = timed(lambda: shard.gather_planes(outs, counts, method=m))  # the exchange alone
+        by[m] = {"op": gather_op_name(m), "us_per_frame": el / reps * 1e6, "blocks_per_s": nblk * reps / el,
+                 "gathered_equals_unsharded": all(bool(torch.equal(f, w)) for f, w in zip(full, want)),
+                 "xgmi": shard.xgmi_report(recv, el_g / reps, world)}
+    first = by[shard.GATHER_METHODS[0]]
+    return {"op": f"one 4K 4:2:0 frame in block-row bands over {world} ranks: forward_quant_planes(bands) + "
+                  f"{first['op']} of the Y/Cb/Cr coefficient planes", "frames": reps,
+            "us_per_frame": first["us_per_frame"], "blocks_per_s": first["blocks_per_s"],
+            "gathered_equals_unsharded": all(v["gathered_equals_unsharded"] for v in by.values()),
+            "xgmi": first["xgmi"], "methods": by}
+
+
+def gather_op_name(method):
+    """What a gather method runs on this process group's backend (bench JSON 'op' strings)."""
+    nccl = dist.get_backend() == "nccl"
+    if method == "p2p":
+        return ("RCCL grouped ncclSend/ncclRecv direct pushes (batch_isend_irecv)" if nccl
+                else f"{dist.get_backend()} isend/irecv direct pushes (batch_isend_irecv)")
+    return "RCCL all_gather_into_tensor" if nccl else f"{dist.get_backend()} all_gather"
 
 
 def gather_leg(args, plan, world, rank, dev):
@@ -399,18 +412,25 @@ def gather_leg(args, plan, world, rank, dev):
         return out
 
     r = shard.strong_gather_leg(forward, frames, counts, args.gather_steps, dev, torch.cuda.synchronize)
-    full, local = r["full"], r["local"]
+    local = r["local"]
     off = sum(counts[:rank])
-    ok = bool(torch.equal(full[off:off + counts[rank]], local))
-    be = "RCCL all_gather_into_tensor" if dist.get_backend() == "nccl" else f"{dist.get_backend()} all_gather"
     n = r["blocks_per_step"] * r["steps"]
-    return {"op": f"{args.total_frames} 4K luma frames split over {world} ranks: forward_quant + {be} of the int16 "
-                  "coefficient planes (BASELINE configs[3])", "scaling": "strong", "world_size": world,
+    recv = (sum(counts) - counts[rank]) * 128
+    by = {m: {"op": gather_op_name(m), "blocks_per_s": n / v["end_to_end_s"],
+              "ms_per_step": v["end_to_end_s"] / r["steps"] * 1e3,
+              "own_slice_intact": bool(torch.equal(v["full"][off:off + counts[rank]], local)),
+              "xgmi": shard.xgmi_report(recv, v["gather_s"] / r["steps"], world)}
+          for m, v in r["by_method"].items()}
+    full0 = r["full"]
+    same = all(bool(torch.equal(v["full"], full0)) for v in r["by_method"].values())
+    first = by[shard.GATHER_METHODS[0]]
+    return {"op": f"{args.total_frames} 4K luma frames split over {world} ranks: forward_quant + {first['op']} of the "
+                  "int16 coefficient planes (BASELINE configs[3])", "scaling": "strong", "world_size": world,
             "frames_total": args.total_frames, "frames_this_rank": hi - lo, "steps": r["steps"],
             "kernel_blocks_per_s": n / r["kernel_s"], "kernel_ms_per_step": r["kernel_s"] / r["steps"] * 1e3,
-            "blocks_per_s": n / r["end_to_end_s"], "ms_per_step": r["end_to_end_s"] / r["steps"] * 1e3,
-            "bytes_received_per_rank": (sum(counts) - counts[rank]) * 128, "own_slice_intact": ok,
-            "xgmi": shard.xgmi_report((sum(counts) - counts[rank]) * 128, r["gather_s"] / r["steps"], world)}
+            "blocks_per_s": first["blocks_per_s"], "ms_per_step": first["ms_per_step"],
+            "bytes_received_per_rank": recv, "own_slice_intact": all(v["own_slice_intact"] for v in by.values()),
+            "methods_gather_the_same": same, "xgmi": first["xgmi"], "methods": by}
 
 
 def small_frame_leg(args, plan, dev):
@@ -701,10 +721,18 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
     """Memory ceilings of the forward kernel's traffic on THIS box, measured in
     rounds beside the forward launch itself, through the diagnostic library
     (libdct_amd_diag.so, csrc/dctq_diag.h):
-      movement_v2 : dctq_diag_movement_planes -- the forward launch's exact data
-                    movement (same grid, prefetch, LDS stage, 1 KiB stores), no math;
+      movement_v3 : dctq_diag_movement_planes -- the product kernel's (fdct8_quant_v3)
+                    exact data movement (same grid, LDS footprint, prefetch, LDS
+                    stage, 1 KiB stores), no math;
+      movement_v2 : dctq_diag_movement_v2_planes -- the same for fdct8_quant_v2 (the
+                    tie-heavy plans' queue kernel), an extra named ceiling;
       flat_1to2_* : dctq_diag_stream 0/1 -- the same byte counts as a flat stream
-                    (16 B per lane, 1 KiB per instruction), nt / default stores;
+                    (16 B per lane, 1 KiB per instruction), nt / default stores,
+                    reading THE SAME PIXEL BYTES (the luma and chroma stacks back to
+                    back): HBM moves constant data faster than random data (up to
+                    9 %), so a ceiling over a constant buffer is not a
+                    ceiling of this workload -- flat_1to2_nt_nt_const shows that
+                    effect and is not a candidate ceiling;
       read_only, write_only(_nt) : dctq_diag_stream 2/3/4 over the same byte counts;
       phased_*    : a read-only launch then a write-only launch, timed as a pair,
                     i.e. the 1:2 traffic with no mix (not reachable by one launch
@@ -724,21 +752,23 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
     pls, outs = [luma, chroma], [coef_y, coef_c]
     nblk = coef_y.shape[0] + coef_c.shape[0]
     nflat = nblk // 64 * 64
-    src = torch.empty(nflat * 64, dtype=torch.uint8, device=dev)
+    src = torch.cat([luma.reshape(-1), chroma.reshape(-1)])[:nflat * 64].contiguous()  # the workload's pixels
+    src7 = torch.full((nflat * 64,), 7, dtype=torch.uint8, device=dev)  # constant data (rounds 1-3's flat input)
     dst = torch.empty(nflat * 128, dtype=torch.uint8, device=dev)
-    src.fill_(7)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def diag_stream(*kinds):
+    def diag_stream(*kinds, buf=src):
         for kind in kinds:
-            rc = D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), nflat, stream)
+            rc = D.dctq_diag_stream(kind, buf.data_ptr(), dst.data_ptr(), nflat, stream)
             if rc:
                 raise RuntimeError(f"dctq_diag_stream({kind}) rc={rc}")
 
     cases = {
         "forward": (lambda: plan.forward_quant_planes(pls, outs=outs), nblk * BYTES_PER_BLOCK),
-        "movement_v2": (lambda: dplan.diag_movement_planes(pls, outs), nblk * BYTES_PER_BLOCK),
+        "movement_v3": (lambda: dplan.diag_movement_planes(pls, outs), nblk * BYTES_PER_BLOCK),
+        "movement_v2": (lambda: dplan.diag_movement_planes(pls, outs, shape=2), nblk * BYTES_PER_BLOCK),
         "flat_1to2_nt_nt": (lambda: diag_stream(0), nflat * BYTES_PER_BLOCK),
+        "flat_1to2_nt_nt_const": (lambda: diag_stream(0, buf=src7), nflat * BYTES_PER_BLOCK),
         "flat_1to2_nt_plain": (lambda: diag_stream(1), nflat * BYTES_PER_BLOCK),
         "read_only": (lambda: diag_stream(2), nflat * 64),
         "write_only": (lambda: diag_stream(3), nflat * 128),
@@ -760,11 +790,11 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
                 times[k].append(e0.elapsed_time(e1) * 1e-3 / b2b)
     med = {k: statistics.median(v) for k, v in times.items()}
     frac = {k: cases[k][1] / med[k] / 1e9 / HBM_PEAK_GBS for k in cases}
-    best = max(("movement_v2", "flat_1to2_nt_nt", "flat_1to2_nt_plain"), key=lambda k: frac[k])
-    del src, dst
+    best = max(("movement_v3", "flat_1to2_nt_nt", "flat_1to2_nt_plain"), key=lambda k: frac[k])
+    del src, src7, dst
     return {"pattern": best, "achieved": frac[best] * HBM_PEAK_GBS, "frac": frac[best],
             "forward_frac": frac["forward"], "forward_over_ceiling": frac["forward"] / frac[best],
-            "forward_over_own_movement": frac["forward"] / frac["movement_v2"], "rounds": rounds,
+            "forward_over_own_movement": frac["forward"] / frac["movement_v3"], "rounds": rounds,
             "launches_per_sample": b2b,
             "hw_ceilings": {k: {"median_us": med[k] * 1e6, "frac": frac[k],
                                 **({"note": "two kernels: an upper bound no single launch that transforms the "

@@ -57,18 +57,21 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
         "dctq_rle_decode": ([vp, vp, ll, vp, vp], i),
         "dctq_huffman_bits": ([vp, ll, vp, vp], i),
         "dctq_huffman_bits_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
+        "dctq_stream_release": ([vp], i),
     }
     if diagnostic:
         sig.update({
             "dctq_diag_plan_set_variant": ([vp, i], i),
             "dctq_diag_plan_set_num_cus": ([vp, i], i),
             "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
+            "dctq_diag_movement_v2_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_rt_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_diag_stream": ([i, vp, vp, ll, vp], i),
             "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
             "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
             "dctq_debug_dc_table": ([i, vp], i),
             "dctq_debug_forward_kernel": ([i, i, ll, i], i),
+            "dctq_diag_stream_stash_bytes": ([vp], ll),
         })
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -229,7 +232,7 @@ class Plan:
                                                _stream_ptr(stream)))
         return outs
 
-    def diag_movement_planes(self, planes, outs, stream=None):
+    def diag_movement_planes(self, planes, outs, stream=None, shape: int = 3):
         """DIAGNOSTIC: the bytes forward_quant_planes moves, with no arithmetic (outs receive
         pixel bytes, not coefficients) -- the memory ceiling of that access pattern."""
         n = len(planes)
@@ -238,7 +241,8 @@ class Plan:
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         if self._L is not _diag:
             raise DctqError("diag_movement_planes needs a plan of the diagnostic library (Plan(..., diagnostic=True))")
-        self._chk(self._L.dctq_diag_movement_planes(self._h, descs, n, C.cast(cp, C.c_void_p), _stream_ptr(stream)))
+        fn = self._L.dctq_diag_movement_planes if shape == 3 else self._L.dctq_diag_movement_v2_planes
+        self._chk(fn(self._h, descs, n, C.cast(cp, C.c_void_p), _stream_ptr(stream)))
         return outs
 
     def diag_rt_movement_planes(self, planes, outs, recons, stream=None):
@@ -341,6 +345,14 @@ class Plan:
                                   C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
                                   n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
         return out
+
+
+def stream_release(stream=None, diagnostic: bool = False) -> None:
+    """dctq_stream_release: wait for `stream` (torch's current one by default) and
+    free the forward's tie-path stashes this thread's launches on it hold (the
+    library that ran them: diagnostic=True for plans of libdct_amd_diag.so)."""
+    L = diag() if diagnostic else lib()
+    _check(L.dctq_stream_release(_stream_ptr(stream)), L)
 
 
 def rle_encode(coef, stream=None):

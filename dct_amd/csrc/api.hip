@@ -10,12 +10,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
+#include <vector>
 
 #include "dct_amd.h"
+#include "dctq_diag.h"
 #include "dctq_internal.h"
 #include "fdct8_bound.h"
 #include "host_tables.h"
@@ -276,41 +280,102 @@ int dctq::plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef,
 // held from the lookup to the kernel launch (stash_guard), so a grow -- which
 // waits for the stream before freeing the smaller stash -- never frees memory a
 // launch enqueued by another thread is about to use.
+//  * The special handles name a different real stream per thread
+//    (hipStreamPerThread always; the null stream under per-thread default-stream
+//    semantics, which a caller may have compiled with): they are keyed by the
+//    calling thread too, so two threads never share a stash through them.
+//  * A launch captured into a graph gets a stash of its OWN, never shared with
+//    direct launches or other captures and never freed by a grow: a replay may
+//    run at any later time, on any stream.  It is allocated in relaxed capture
+//    mode (no stream work) and released by dctq_stream_release.
 namespace {
 struct Stash {
     void *ptr = nullptr;
     size_t bytes = 0;
 };
+struct StreamStash {
+    Stash live;                   // direct launches on this stream
+    std::vector<void *> captured;  // one per captured launch, kept until dctq_stream_release
+};
+struct StashKey {
+    int device;
+    hipStream_t stream;
+    std::thread::id thread;  // default-constructed (no thread) for ordinary streams
+    bool operator<(const StashKey &o) const {
+        if (device != o.device) return device < o.device;
+        if (stream != o.stream) return std::less<hipStream_t>()(stream, o.stream);
+        return thread < o.thread;
+    }
+};
 std::mutex g_stash_mu;
-std::map<std::pair<int, hipStream_t>, Stash> g_stash;
+std::map<StashKey, StreamStash> g_stash;
 struct StashCtx {
     int device;
     hipStream_t stream;
     hipError_t err;
 };
 
+StashKey stash_key(int device, hipStream_t stream) {
+    const bool per_thread = stream == nullptr || stream == hipStreamPerThread;
+    return StashKey{device, stream, per_thread ? std::this_thread::get_id() : std::thread::id()};
+}
+
 void *stash_for(void *vctx, size_t bytes) {  // called with g_stash_mu held
     StashCtx &c = *static_cast<StashCtx *>(vctx);
-    Stash &s = g_stash[{c.device, c.stream}];
-    if (s.bytes >= bytes) return s.ptr;
+    StreamStash &s = g_stash[stash_key(c.device, c.stream)];
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(c.stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
-        c.err = hipErrorStreamCaptureUnsupported;  // run the launch once before capturing it
-        return nullptr;
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+        void *p = nullptr;
+        c.err = hipMalloc(&p, bytes);
+        (void)hipThreadExchangeStreamCaptureMode(&mode);  // restore the caller's mode
+        if (c.err != hipSuccess) return nullptr;
+        s.captured.push_back(p);
+        return p;
     }
-    if (s.ptr) {
+    if (s.live.bytes >= bytes) return s.live.ptr;
+    if (s.live.ptr) {
         if ((c.err = hipStreamSynchronize(c.stream)) != hipSuccess) return nullptr;
-        (void)hipFree(s.ptr);
-        s = Stash{};
+        (void)hipFree(s.live.ptr);
+        s.live = Stash{};
     }
-    if ((c.err = hipMalloc(&s.ptr, bytes)) != hipSuccess) {
-        s = Stash{};
+    if ((c.err = hipMalloc(&s.live.ptr, bytes)) != hipSuccess) {
+        s.live = Stash{};
         return nullptr;
     }
-    s.bytes = bytes;
-    return s.ptr;
+    s.live.bytes = bytes;
+    return s.live.ptr;
 }
 }  // namespace
+
+extern "C" {
+
+int dctq_stream_release(void *stream) {
+    DCTQ_ENTRY;
+    int dev = -1;
+    HIPCHK(hipGetDevice(&dev), "hipGetDevice");
+    std::lock_guard<std::mutex> stash_guard(g_stash_mu);
+    auto it = g_stash.find(stash_key(dev, (hipStream_t)stream));
+    if (it == g_stash.end()) return DCTQ_OK;
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
+    (void)hipFree(it->second.live.ptr);
+    for (void *p : it->second.captured) (void)hipFree(p);
+    g_stash.erase(it);
+    return DCTQ_OK;
+}
+
+long long dctq_diag_stream_stash_bytes(void *stream) {
+    DCTQ_ENTRY;
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> stash_guard(g_stash_mu);
+    auto it = g_stash.find(stash_key(dev, (hipStream_t)stream));
+    if (it == g_stash.end()) return 0;
+    return (long long)it->second.live.bytes;
+}
+
+}  // extern "C"
 
 extern "C" {
 
@@ -329,9 +394,6 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
                                      plan->variant, plan->num_cus, dctq::RingSource{stash_for, &sc},
                                      plan->host.quant[0] <= 1.0);  // the same test as dctq_debug_forward_kernel
     }
-    if (sc.err == hipErrorStreamCaptureUnsupported)
-        return fail(DCTQ_EINVAL, "the tie-path stash of this stream is smaller than this launch needs: run the launch "
-                                 "once on the stream before capturing it");
     if (sc.err != hipSuccess) return fail(DCTQ_ENOMEM, "tie-path stash", sc.err);
     HIPCHK(e, "fdct8_quant launch");
     return DCTQ_OK;

@@ -25,12 +25,17 @@ int dctq_diag_plan_set_variant(dctq_plan *plan, int variant);
  * batch of a 4K frame stack, so its row carry between batches runs only then). */
 int dctq_diag_plan_set_num_cus(dctq_plan *plan, int num_cus);
 
-/* Moves exactly the bytes dctq_forward_quant_planes moves (same grid, prefetch,
- * LDS stage and 1 KiB stores) with no arithmetic.  coef[k] receives pixel bytes,
+/* Moves exactly the bytes dctq_forward_quant_planes moves, in the access pattern
+ * of its product kernel fdct8_quant_v3 (same grid, LDS footprint, prefetch, LDS
+ * stage and 1 KiB stores) with no arithmetic.  coef[k] receives pixel bytes,
  * NOT coefficients.  Its time is the memory ceiling of the forward kernel's own
  * access pattern. */
 int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               void *stream);
+/* The same in the access pattern of fdct8_quant_v2 (the tie-heavy plans' queue
+ * kernel: its queue arrays in LDS, its first-batch loads). */
+int dctq_diag_movement_v2_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                 void *stream);
 
 /* The same for the fused round trip (dctq_round_trip_planes): its grid, stage
  * and stores with no arithmetic; coef[k] and recon[k] receive pixel bytes. */
@@ -50,6 +55,10 @@ int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes
  * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kind 5: blocks * 384),
  * both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
+
+/* Bytes of the tie-path stash the calling thread's launches on `stream` use for
+ * direct (uncaptured) forward launches; 0 if none (tests of dctq_stream_release). */
+long long dctq_diag_stream_stash_bytes(void *stream);
 
 /* Host-only introspection for the CPU tests (no GPU needed). */
 /* The forward kernel (1, 2, 3 = fdct8_quant_v1/v2/v3) dctq_forward_quant_planes runs

@@ -134,8 +134,9 @@ hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const Dev
 int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy);
 // bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
 size_t fdct8_ring_bytes(int workgroups);
-// diagnostic: fdct8_quant_v2's data movement without arithmetic (fdct8.hip)
-hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num_cus);
+// diagnostic: the forward's data movement without arithmetic (fdct8.hip): shape 3 =
+// fdct8_quant_v3's (the product kernel), 2 = fdct8_quant_v2's (the tie-heavy plans' queue kernel)
+hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape);
 hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
                             hipStream_t stream, int num_cus);
 // diagnostic: roundtrip8's data movement without arithmetic (roundtrip.hip)

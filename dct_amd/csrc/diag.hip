@@ -108,7 +108,17 @@ int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, i
     if (int rc = dctq::check_plan(plan)) return rc;
     dctq::PlaneSet ps;
     if (int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &ps)) return rc;
-    HIPCHK(dctq::launch_fdct8_movement(ps, (hipStream_t)stream, plan->num_cus), "fdct8_movement launch");
+    HIPCHK(dctq::launch_fdct8_movement(ps, plan->dev, (hipStream_t)stream, plan->num_cus, 3), "fdct8_movement launch");
+    return DCTQ_OK;
+}
+
+int dctq_diag_movement_v2_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                 void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = dctq::check_plan(plan)) return rc;
+    dctq::PlaneSet ps;
+    if (int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &ps)) return rc;
+    HIPCHK(dctq::launch_fdct8_movement(ps, plan->dev, (hipStream_t)stream, plan->num_cus, 2), "fdct8_movement_v2 launch");
     return DCTQ_OK;
 }
 

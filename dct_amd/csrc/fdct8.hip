@@ -591,12 +591,61 @@ int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy
 }
 
 // ============================================================================
-// Diagnostic: the v2 kernel's data movement with no arithmetic (the memory
-// ceiling of this exact access pattern, measured on the same box as the
-// kernel -- bench.py reports kernel time / this time).  Same persistent grid,
-// occupancy, prefetch, LDS stage, fence and 1 KiB non-temporal stores as
-// fdct8_batch; the "coefficients" are the pixel rows twice over.
-__global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps) {
+// Diagnostics: the forward kernels' data movement with no arithmetic (the
+// memory ceiling of their exact access patterns, measured on the same box as
+// the kernel -- bench.py reports kernel time / movement time).  Same grid,
+// occupancy (LDS footprint), prefetch, LDS stage, fence and 1 KiB
+// non-temporal stores as the kernel; the "coefficients" are the pixel rows
+// twice over.
+//  fdct8_movement     -- fdct8_quant_v3, the product kernel: its LDS (stage, 1 KiB
+//                        exact tables loaded at start, 512 B of entries), its
+//                        prefetch (nothing past the end), its 32 b32 stage writes
+//                        per lane and its stage read-back;
+//  fdct8_movement_v2  -- fdct8_quant_v2 (the tie-heavy plans' queue kernel): its
+//                        queue arrays and first-batch load_rows.
+__global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, const DevTables *__restrict__ dev) {
+    __shared__ uint4 stage[kFThreads * kPitch2 / 16];
+    __shared__ ExactTables tab;
+    __shared__ uint16_t scr[kFWaves * 64];
+    load_exact_tables(&tab, dev);
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (ps.n < 0) scr[threadIdx.x] = (uint16_t)tab.dct[lane];  // keep the footprint allocated
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t step = gridDim.x * kFWaves;
+    uint32_t g = blockIdx.x * kFWaves + wv;
+    uint2 nxt[8];
+    prefetch_batch(ps, g, lane, nxt);
+    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    for (; g < nbatch; g += step) {
+        const int k = plane_of(ps, g);
+        const PlaneArgs &p = ps.pl[k];
+        const uint32_t b = g - ps.first[k];
+        uint2 cur[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+        prefetch_batch(ps, g + step, lane, nxt);
+        // fdct8_compute's stage writes: dword i*4 + cp of the lane's 136-B slot
+        uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
+#pragma unroll
+        for (int cp = 0; cp < 4; ++cp)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) st32[i * 4 + cp] = cp & 1 ? cur[i].y : cur[i].x ^ (uint32_t)cp;
+        asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                     "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+        wave_sync();
+        u4v val[8];
+        stage_chunks(stage, wv, lane, val);
+        const uint32_t left = (uint32_t)p.nblk - b * 64;
+        const uint32_t nb = left < 64u ? left : 64u;
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<char *>(coef_of(ps, k)) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_STORE_AUX);
+    }
+}
+
+__global__ __launch_bounds__(kFThreads, 4) void fdct8_movement_v2(PlaneSet ps) {
     __shared__ uint4 stage[kFThreads * kPitch2 / 16];
     __shared__ uint32_t qpad[kFWaves * kQCap];   // same LDS footprint as fdct8_quant_v2
     __shared__ uint16_t qpad2[kFWaves * kQCap];  // (occupancy is LDS-bound)
@@ -628,33 +677,30 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps) {
         }
         asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                      "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
         const uint32_t left = (uint32_t)p.nblk - b * 64;
         const uint32_t nb = left < 64u ? left : 64u;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             reinterpret_cast<char *>(coef_of(ps, k)) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
-        const uint2 *st64 = reinterpret_cast<const uint2 *>(stage) + wv * 64 * (kPitch2 / 8);
         u4v val[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int m = q * 64 + lane;
-            const int bl = m >> 3;
-            const uint2 lo = st64[bl * (kPitch2 / 8) + (m & 7) * 2], hi = st64[bl * (kPitch2 / 8) + (m & 7) * 2 + 1];
-            val[q] = u4v{lo.x, lo.y, hi.x, hi.y};
-        }
+        stage_chunks(stage, wv, lane, val);
 #pragma unroll
         for (int q = 0; q < 8; ++q) __builtin_amdgcn_raw_buffer_store_b128(val[q], rs, lane * 16, q * 1024, DCTQ_STORE_AUX);
     }
 }
 
-hipError_t launch_fdct8_movement(const PlaneSet &ps, hipStream_t stream, int num_cus) {
-    static const int per_cu = resident_per_cu(fdct8_movement, kFThreads);
+hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape) {
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_v2
-    hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps);
+    if (shape == 2) {
+        static const int per_cu = resident_per_cu(fdct8_movement_v2, kFThreads);
+        const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_v2
+        hipLaunchKernelGGL(fdct8_movement_v2, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps);
+    } else {
+        static const int per_cu = resident_per_cu(fdct8_movement, kFThreads);
+        const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_v3
+        hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps, dev);
+    }
     return hipGetLastError();
 }
 }  // namespace dctq

@@ -12,10 +12,20 @@ The only collectives are OPTIONAL gathers: of the int16 coefficient planes
 (BASELINE configs[3]: "RCCL allgather of quantized coefficient planes over
 xGMI"; several planes of a frame in one message with gather_planes), or of the
 run-length symbol streams the encoder makes of them (shrink the
-bytes before the exchange).  Each is one all_gather per call over the whole
-shard, padded to the largest shard so ragged splits work.  The
-ordering of the gathered result equals the unsharded raster order, so rank r's
-slice lands at blocks_before(r).
+bytes before the exchange).  The ordering of the gathered result equals the
+unsharded raster order, so rank r's slice lands at blocks_before(r).
+
+The coefficient gathers come in SURVEY 8(e)'s two shapes (`method`):
+  "all_gather" -- one all_gather_into_tensor per call over the whole shard,
+                  padded to the largest shard so ragged splits work (RCCL picks
+                  its algorithm: a ring takes in one xGMI link per step);
+  "p2p"        -- direct pushes: every rank sends its shard to each of the
+                  N - 1 peers and receives each peer's shard straight into its
+                  slot of the output, all 2 (N - 1) transfers in ONE group
+                  (dist.batch_isend_irecv = ncclGroupStart / ncclSend x (N-1) /
+                  ncclRecv x (N-1) / ncclGroupEnd), so all 7 links of an MI355X
+                  node carry data at once; no padding and no compaction copy.
+The gathered tensors are identical either way (tests/test_shard.py).
 """
 from __future__ import annotations
 
@@ -45,19 +55,80 @@ def band_shard(px, world: int, rank: int):
     return px[..., 8 * lo:8 * hi, :], (lo, hi - lo)
 
 
-def gather_coefficients(local, counts, group=None):
-    """All-gather int16 coefficient shards [n_r, 64] (n_r = counts[r]) into the
-    full [sum(counts), 64] tensor on every rank, in rank order.
+GATHER_METHODS = ("all_gather", "p2p")
 
-    One collective over the whole shard (bigger messages, fewer calls: xGMI
-    rings are per-link bound).  Ragged shards are padded to
-    max(counts) and compacted after the exchange."""
+
+def _check_method(method):
+    if method not in GATHER_METHODS:
+        raise ValueError(f"gather method must be one of {GATHER_METHODS}")
+
+
+def _wire(t):
+    """The bytes of a contiguous tensor as uint8 (RCCL has no int16; gloo moves raw bytes)."""
+    import torch
+    return t.reshape(-1).view(torch.uint8)
+
+
+def gather_p2p(locals_, counts, group=None):
+    """Direct-push gather of several planes' shards (SURVEY 8(e) "grouped
+    ncclSend/ncclRecv"): locals_[p] is this rank's [counts[p][rank], ...] shard
+    of plane p.  Every rank pushes each of its shards to every peer and receives
+    every peer's shard directly into its row range of the per-plane output
+    ([sum(counts[p]), ...], rank order), all transfers in one
+    dist.batch_isend_irecv group -- N - 1 concurrent peer links, no padding,
+    no staging buffer, no compaction.  Empty shards send nothing (both ends
+    skip them).  The own shard is a device copy."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if len(locals_) != len(counts) or not locals_:
+        raise ValueError("one counts list per plane")
+    # gloo's send/recv move host memory only: device shards travel through host copies there
+    # (the rehearsal of the N>1 legs on one GPU); RCCL moves them device to device over xGMI
+    host = dist.get_backend(group) != "nccl" and locals_[0].device.type != "cpu"
+    fulls, ops = [], []
+    for loc, c in zip(locals_, counts):
+        if len(c) != world or loc.shape[0] != c[rank]:
+            raise ValueError("counts must list every rank's shard size of every plane")
+        offs = [0]
+        for n in c:
+            offs.append(offs[-1] + n)
+        dev = torch.device("cpu") if host else loc.device
+        full = torch.empty((offs[-1],) + tuple(loc.shape[1:]), dtype=loc.dtype, device=dev)
+        src = loc.to(dev).contiguous()
+        full[offs[rank]:offs[rank + 1]].copy_(src)
+        for d in range(1, world):  # peers in ring order from this rank: every link busy at once
+            to, frm = (rank + d) % world, (rank - d) % world
+            if c[rank]:
+                ops.append(dist.P2POp(dist.isend, _wire(src), to, group))
+            if c[frm]:
+                ops.append(dist.P2POp(dist.irecv, _wire(full[offs[frm]:offs[frm + 1]]), frm, group))
+        fulls.append(full)
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    if host:
+        fulls = [f.to(loc.device) for f, loc in zip(fulls, locals_)]
+    return fulls
+
+
+def gather_coefficients(local, counts, group=None, method="all_gather"):
+    """All-gather int16 coefficient shards [n_r, 64] (n_r = counts[r]) into the
+    full [sum(counts), 64] tensor on every rank, in rank order.
+
+    method "all_gather": one collective over the whole shard (bigger messages,
+    fewer calls), ragged shards padded to max(counts) and compacted after the
+    exchange.  method "p2p": gather_p2p's direct pushes."""
+    import torch
+    import torch.distributed as dist
+    _check_method(method)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     if len(counts) != world or local.shape[0] != counts[rank]:
         raise ValueError("counts must list every rank's shard size")
+    if method == "p2p":
+        return gather_p2p([local], [counts], group)[0]
     m = max(counts)
     if local.shape[0] < m:
         pad = torch.zeros((m - local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
@@ -81,15 +152,20 @@ def gather_coefficients(local, counts, group=None):
     return torch.cat([p[:c] for p, c in zip(parts, counts)])
 
 
-def gather_planes(locals_, counts, group=None):
+def gather_planes(locals_, counts, group=None, method="all_gather"):
     """All-gather the coefficient shards of SEVERAL planes (e.g. a frame's Y, Cb
     and Cr bands: locals_[p] is [counts[p][rank], 64]) in ONE collective: every
     plane's shard padded to its largest rank, concatenated, exchanged, and split
     back into per-plane [sum(counts[p]), 64] tensors in rank order.  One message
     instead of one per plane: each collective pays the RCCL launch and ring
-    latency, and a 4K frame's band is only ~2-4 MB per rank at N = 8."""
+    latency, and a 4K frame's band is only ~2-4 MB per rank at N = 8.
+    method "p2p": every plane's shard pushed to every peer in one group
+    (gather_p2p), received in place."""
     import torch
     import torch.distributed as dist
+    _check_method(method)
+    if method == "p2p":
+        return gather_p2p(locals_, counts, group)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if len(locals_) != len(counts) or not locals_:
@@ -182,21 +258,26 @@ def max_over_ranks(seconds: float, device, group=None) -> float:
     return float(t.item())
 
 
-def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: None, group=None) -> dict:
+def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: None, group=None,
+                      methods=GATHER_METHODS) -> dict:
     """BASELINE configs[3]: a fixed batch of frames split over the ranks
     (strong scaling; `frames` is this rank's frame_shard), forward DCT+quant of
-    the shard, then the coefficient planes all-gathered onto every rank.
+    the shard, then the coefficient planes gathered onto every rank.
 
     forward(frames) -> int16 [counts[rank], 64] (the device kernel on the GPU,
-    anything equivalent in the CPU tests); `sync` waits for the device.  Two
-    timed loops of `steps` steps, each bracketed by a barrier and `sync`, the
-    time the max over ranks:
+    anything equivalent in the CPU tests); `sync` waits for the device.  Timed
+    loops of `steps` steps, each bracketed by a barrier and `sync`, the time the
+    max over ranks:
       kernel-only : forward alone -> the aggregate rate of the GPUs' kernels;
+    and for each gather method (GATHER_METHODS: the all-gather collective and
+    the direct peer pushes, SURVEY 8(e)'s two shapes):
       end-to-end  : forward + gather_coefficients -> what a caller that needs
                     every coefficient on every rank gets (xGMI-bound);
       gather-only : gather_coefficients of the shard already computed -> the
                     exchange alone, for its achieved bytes per second per rank.
-    Returns the three times, the blocks per step and the last gathered tensor."""
+    Returns the times (the first method's under the plain keys, every method's
+    under by_method[m]), the blocks per step and the last gathered tensor of
+    each method (full = the first method's)."""
     import time
     import torch.distributed as dist
     total = sum(counts)
@@ -212,11 +293,17 @@ def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: 
         sync()
         return max_over_ranks(time.perf_counter() - t0, device, group), out
 
+    for m in methods:
+        _check_method(m)
     t_kernel, local = timed(lambda: forward(frames))
-    t_e2e, full = timed(lambda: gather_coefficients(forward(frames), counts, group))
-    t_gather, _ = timed(lambda: gather_coefficients(local, counts, group))
-    return {"blocks_per_step": total, "steps": steps, "kernel_s": t_kernel, "end_to_end_s": t_e2e,
-            "gather_s": t_gather, "local": local, "full": full}
+    by = {}
+    for m in methods:
+        t_e2e, full = timed(lambda: gather_coefficients(forward(frames), counts, group, m))
+        t_gather, _ = timed(lambda: gather_coefficients(local, counts, group, m))
+        by[m] = {"end_to_end_s": t_e2e, "gather_s": t_gather, "full": full}
+    first = by[methods[0]]
+    return {"blocks_per_step": total, "steps": steps, "kernel_s": t_kernel, "end_to_end_s": first["end_to_end_s"],
+            "gather_s": first["gather_s"], "local": local, "full": first["full"], "by_method": by}
 
 
 # xGMI on an MI355X node is point-to-point, 7 links of ~153 GB/s per

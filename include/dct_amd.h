@@ -48,7 +48,11 @@ typedef struct dctq_plan dctq_plan;
  * batches than the device has resident waves; other plans resolve their ties in
  * place), sized to that launch's grid (8 KiB per wave,
  * at most 256 MiB on a 256-CU MI355X) and kept for later launches on the same
- * stream.  Under hipGraph capture, run the launch once on the stream first. */
+ * stream until dctq_stream_release.  The NULL stream and hipStreamPerThread
+ * get one stash per calling thread (each thread's real stream differs).  A
+ * launch captured into a hipGraph gets a stash of its own, never shared and
+ * never reallocated, so replays may run at any time on any stream; it lives
+ * until dctq_stream_release of the capture stream. */
 int dctq_plan_create(int quality, int adaptive, dctq_plan **plan);
 /* Bind an existing reference-style context (block_size must be 8); its
  * quant_matrix VALUES are used, so a caller-modified table is honoured. */
@@ -159,6 +163,13 @@ int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, vo
  * never leave the chip.  bits: 4-byte aligned, one entry per block. */
 int dctq_huffman_bits_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *bits,
                              void *stream);
+
+/* Waits for `stream` and frees the tie-path stashes the calling thread's
+ * forward launches on it hold (the direct one and every captured launch's):
+ * call it before destroying a stream that ran tie-heavy forwards, and only
+ * after the last replay of any graph captured on it.  A later launch on the
+ * stream allocates a new stash.  No-op for a stream that holds none. */
+int dctq_stream_release(void *stream);
 
 /* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented
  * by the number of coefficients resolved by the exact fp64 tie path in later

@@ -320,6 +320,92 @@ def test_plans_cheap_and_stash_per_stream(T, dm):
     assert np.array_equal(outs[1].cpu().numpy(), want)
 
 
+class _PerThreadStream:
+    """hipStreamPerThread as a stream argument: one handle value (2), a different real stream per thread."""
+    cuda_stream = 2
+
+
+def test_stash_per_thread_stream_two_threads(T, dm):
+    """hipStreamPerThread is one handle value but a different real
+    stream on each thread.  Two threads run a tie-heavy plan (q99, the v2 queue
+    kernel with its pixel stash, 4 batches per wave) concurrently on it: each
+    thread's launches get their own stash, so both outputs equal the oracle;
+    dctq_stream_release from each thread frees that thread's stash only."""
+    import threading
+    import oracle as O
+    px = dm.synth(5151, "uniform", 3840, 2160, 2)
+    host = px.cpu().numpy()
+    want = np.concatenate([O.forward_plane(host[f], 99, 0, 8) for f in range(2)])
+    plan = dm.Plan(99, 0, variant=4, num_cus=8)  # v2 forced; 1 024 waves for 4 050 batches
+    outs = [T.zeros((2 * 480 * 270, 64), dtype=T.int16, device="cuda") for _ in range(2)]
+    T.cuda.synchronize()
+    L = dm.diag()
+    errs, sizes = [], [0, 0]
+    start = threading.Barrier(2)
+
+    def work(k):
+        try:
+            start.wait()
+            for _ in range(4):
+                plan.forward_quant(px, out=outs[k], stream=_PerThreadStream())
+            dm._check(L.dctq_synchronize(C.c_void_p(2)), L)
+            sizes[k] = L.dctq_diag_stream_stash_bytes(C.c_void_p(2))
+            dm.stream_release(_PerThreadStream(), diagnostic=True)
+            assert L.dctq_diag_stream_stash_bytes(C.c_void_p(2)) == 0
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    assert sizes[0] > 0 and sizes[1] > 0, sizes  # each thread had its own stash
+    for k in range(2):
+        got = outs[k].cpu().numpy()
+        assert np.array_equal(got, want), (k, int((got != want).sum()))
+
+
+def test_stash_captured_launch_survives_grow(T, dm):
+    """a forward captured into a graph keeps a stash of its own.  A
+    small tie-heavy launch (q99, v2) is captured, then a LARGER direct launch on the
+    same stream grows (frees and reallocates) the stream's stash, then the graph
+    is replayed: its output still equals the oracle.  Released at the end."""
+    import oracle as O
+    small = dm.synth(6161, "uniform", 1920, 1080, 2)
+    big = dm.synth(6262, "uniform", 3840, 2160, 2)
+    plan_small = dm.Plan(99, 1, variant=4, num_cus=2)  # a small grid: a small stash
+    plan_big = dm.Plan(99, 1, variant=4, num_cus=64)  # a larger grid: grows the stream's stash
+    out_s = T.zeros((2 * 240 * 135, 64), dtype=T.int16, device="cuda")
+    out_b = T.zeros((2 * 480 * 270, 64), dtype=T.int16, device="cuda")
+    s = T.cuda.Stream()
+    s.wait_stream(T.cuda.current_stream())
+    with T.cuda.stream(s):
+        plan_small.forward_quant(small, out=out_s, stream=s)  # a live stash sized for the small grid
+    s.synchronize()
+    g = T.cuda.CUDAGraph()
+    with T.cuda.graph(g, stream=s):
+        plan_small.forward_quant(small, out=out_s, stream=s)
+    L = dm.diag()
+    before = L.dctq_diag_stream_stash_bytes(C.c_void_p(s.cuda_stream))
+    with T.cuda.stream(s):
+        plan_big.forward_quant(big, out=out_b, stream=s)
+    s.synchronize()
+    assert L.dctq_diag_stream_stash_bytes(C.c_void_p(s.cuda_stream)) > before > 0
+    out_s.zero_()
+    T.cuda.synchronize()
+    g.replay()
+    g.replay()
+    T.cuda.synchronize()
+    hs, hb = small.cpu().numpy(), big.cpu().numpy()
+    assert np.array_equal(out_s.cpu().numpy(), np.concatenate([O.forward_plane(hs[f], 99, 1, 8) for f in range(2)]))
+    assert np.array_equal(out_b.cpu().numpy(), np.concatenate([O.forward_plane(hb[f], 99, 1, 8) for f in range(2)]))
+    del g
+    dm.stream_release(s, diagnostic=True)
+    assert L.dctq_diag_stream_stash_bytes(C.c_void_p(s.cuda_stream)) == 0
+
+
 def test_bench_gpus2_gloo(T, dm):
     """bench.py --gpus 2 with no launcher forms a 2-rank world by itself (its
     children share this box's one GPU over gloo, as a rehearsal of the driver's
@@ -346,6 +432,10 @@ def test_bench_gpus2_gloo(T, dm):
     assert b["gathered_equals_unsharded"] is True, b
     assert g["xgmi"]["bytes_received_per_rank"] == g["bytes_received_per_rank"] > 0, g
     assert b["xgmi"]["achieved_GBs_per_rank"] > 0, b
+    # the direct-push shape at world 2: the same coefficients as the all-gather, band equal to unsharded
+    assert g["methods_gather_the_same"] is True and g["methods"]["p2p"]["own_slice_intact"] is True, g
+    assert b["methods"]["p2p"]["gathered_equals_unsharded"] is True, b
+    assert g["methods"]["p2p"]["xgmi"]["bytes_received_per_rank"] == g["bytes_received_per_rank"], g
 
 
 def test_dist_legs_rccl_one_rank(T, dm):
@@ -368,6 +458,13 @@ def test_dist_legs_rccl_one_rank(T, dm):
     g, b, e = d["gather"], d["band"], d["encode"]
     assert "RCCL" in g["op"] and g["own_slice_intact"] and g["world_size"] == 1, g
     assert "RCCL" in b["op"] and b["gathered_equals_unsharded"], b
+    # both of SURVEY 8(e)'s shapes ran through RCCL: the all-gather and the grouped send/recv pushes
+    for leg in (g, b):
+        assert set(leg["methods"]) == {"all_gather", "p2p"}, leg
+        assert "ncclSend/ncclRecv" in leg["methods"]["p2p"]["op"], leg
+        assert leg["methods"]["p2p"]["xgmi"]["us_per_gather"] > 0, leg
+    assert g["methods_gather_the_same"] and g["methods"]["p2p"]["own_slice_intact"], g
+    assert b["methods"]["p2p"]["gathered_equals_unsharded"], b
     assert "RCCL" in e["gather_op"] and e["gather_blocks_per_s"] > 0, e
 
 

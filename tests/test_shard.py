@@ -37,9 +37,10 @@ def _worker(rank, world, port, q):
                                  if hi > lo else np.zeros((0, 64), np.int16))
         per = (48 // 8) * (40 // 8)
         counts = [(shard.split(5, world, r)[1] - shard.split(5, world, r)[0]) * per for r in range(world)]
-        full = shard.gather_coefficients(local, counts)
         want = np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in frames])
-        assert np.array_equal(full.numpy(), want), "frame-sharded gather differs"
+        for method in shard.GATHER_METHODS:  # the all-gather collective and the direct peer pushes
+            full = shard.gather_coefficients(local, counts, method=method)
+            assert np.array_equal(full.numpy(), want), f"frame-sharded gather differs ({method})"
 
         # (2) block-row bands of one plane: 7 block rows, adaptive, q90
         plane = torch.from_numpy(O.synth_plane(99, O.KINDS["smooth"], 64, 56))
@@ -47,8 +48,9 @@ def _worker(rank, world, port, q):
         local = torch.from_numpy(O.forward_plane(np.ascontiguousarray(band.numpy()), 90, 1)
                                  if rows else np.zeros((0, 64), np.int16))
         counts = [shard.split(7, world, r)[1] * 8 - shard.split(7, world, r)[0] * 8 for r in range(world)]
-        full = shard.gather_coefficients(local, counts)
-        assert np.array_equal(full.numpy(), O.forward_plane(plane.numpy(), 90, 1)), "band-sharded gather differs"
+        for method in shard.GATHER_METHODS:
+            full = shard.gather_coefficients(local, counts, method=method)
+            assert np.array_equal(full.numpy(), O.forward_plane(plane.numpy(), 90, 1)), f"band gather differs ({method})"
 
         # (2b) a frame's three planes in block-row bands, gathered in ONE collective (bench's band leg)
         planes = [O.synth_plane(500 + k, O.KINDS[kind], w, h)
@@ -60,9 +62,21 @@ def _worker(rank, world, port, q):
                                          if rows else np.zeros((0, 64), np.int16)))
             bh = pl.shape[0] // 8
             cnts.append([(b - a) * (pl.shape[1] // 8) for a, b in (shard.split(bh, world, r) for r in range(world))])
-        fulls = shard.gather_planes(locs, cnts)
-        for pl, f in zip(planes, fulls):
-            assert np.array_equal(f.numpy(), O.forward_plane(pl, 50, 0)), "multi-plane band gather differs"
+        for method in shard.GATHER_METHODS:
+            fulls = shard.gather_planes(locs, cnts, method=method)
+            for pl, f in zip(planes, fulls):
+                assert np.array_equal(f.numpy(), O.forward_plane(pl, 50, 0)), f"multi-plane band gather differs ({method})"
+
+        # (2c) direct pushes with EMPTY shards on some ranks (a 1-block-row plane: only rank 0 holds rows)
+        tiny = O.synth_plane(901, O.KINDS["uniform"], 40, 8)
+        band, (row0, rows) = shard.band_shard(torch.from_numpy(tiny), world, rank)
+        local = torch.from_numpy(O.forward_plane(np.ascontiguousarray(band.numpy()), 50, 0)
+                                 if rows else np.zeros((0, 64), np.int16))
+        counts = [(b - a) * 5 for a, b in (shard.split(1, world, r) for r in range(world))]
+        full = shard.gather_coefficients(local, counts, method="p2p")
+        assert np.array_equal(full.numpy(), O.forward_plane(tiny, 50, 0)), "p2p gather with empty shards differs"
+        with pytest.raises(ValueError):
+            shard.gather_coefficients(local, counts, method="ring")
 
         # (3) run-length streams of the frame shards (what dctq_encode_planes makes on each GPU)
         mine, (lo, hi) = shard.frame_shard(frames, world, rank)
@@ -90,6 +104,10 @@ def _worker(rank, world, port, q):
         r = shard.strong_gather_leg(forward, stack[lo:hi], counts, 2, torch.device("cpu"))
         assert r["blocks_per_step"] == total * per and r["steps"] == 2
         assert r["kernel_s"] > 0 and r["end_to_end_s"] > 0 and r["gather_s"] > 0
+        assert set(r["by_method"]) == set(shard.GATHER_METHODS)
+        for m, rm in r["by_method"].items():  # both shapes timed, both gather the same coefficients
+            assert rm["end_to_end_s"] > 0 and rm["gather_s"] > 0
+            assert torch.equal(rm["full"], r["full"]), m
         x = shard.xgmi_report((total * per - counts[rank]) * 128, r["gather_s"] / r["steps"], world)
         assert x["bytes_received_per_rank"] == (total * per - counts[rank]) * 128
         assert x["direct_estimate_GBs"] == (world - 1) * shard.XGMI_LINK_GBS

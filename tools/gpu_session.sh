@@ -48,6 +48,9 @@ for step in "$@"; do
     mix2) run mix2 300 tools/ubench/hbm_mix2 10 ;;
     mix3) run mix3 300 tools/ubench/hbm_mix3 10 ;;
     mix4) run mix4 300 tools/ubench/hbm_mix4 10 ;;
+    move5a) run move5a 180 tools/ubench/move5 12 3 ;;
+    testnew) run pytest_new 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "stash or dist_legs or gpus2 or bench_json" ;;
+    move5b) run move5b 180 tools/ubench/move5 12 3 ;;
     phase) run phase 120 tools/ubench/hbm_phase 8 ;;
     planes) run planes 300 python tools/plane_bench.py ;;
     legacy) run legacy 120 host/legacy_latency ;;
