@@ -20,6 +20,10 @@
 #include "fdct8_core.h"
 #include "scan_core.h"
 
+#ifndef DCTQ_ENC_GRID_MULT
+#define DCTQ_ENC_GRID_MULT DCTQ_GRID_MULT  // grid multiplier of this file's streaming kernels (dctq_internal.h)
+#endif
+
 namespace dctq {
 
 __device__ __forceinline__ void fence_rows(uint2 (&nxt)[8]) {
@@ -93,7 +97,7 @@ template <typename K, typename... A>
 static hipError_t launch_enc(K kernel, uint32_t nbatch, int num_cus, hipStream_t stream, A... args) {
     const int per_cu = resident_per_cu(kernel, kThreads);
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_ENC_GRID_MULT);
     hipLaunchKernelGGL(kernel, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, args...);
     return hipGetLastError();
 }

@@ -503,6 +503,15 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 #ifndef DCTQ_V3_GROUP8
 #define DCTQ_V3_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped8)
 #endif
+#ifndef DCTQ_V3_GRID_MULT
+// fdct8_quant_v3 launches 16 x its resident workgroups (round 4, profiles/r04/forward_grid_sweep.log,
+// one box, interleaved, two passes: x8 424.6 / 424.0 us, x12 417.1 / 416.1, x16 413.3 / 412.1,
+// x24 416.9 / 417.6, x32 424.0 / 421.0, x48 (one batch per wave) 428.4 / 427.4 on the bench step;
+// x16 also -1.8 % extreme q10, -3.5 % smooth q90 adaptive, +0.5 % constant blocks).  With no stash
+// (v3 resolves ties in place) the grid costs nothing but workgroup starts; round 2's x16 regression
+// was the v2 queue kernel's.
+#define DCTQ_V3_GRID_MULT 16
+#endif
 #ifndef DCTQ_FWD_INPLACE
 #define DCTQ_FWD_INPLACE 1  // the product dispatch picks v3 (in-place ties) at every size unless the plan is tie-heavy
 #endif
@@ -523,13 +532,14 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
     uint32_t resolved = 0;
     for (; g < nbatch; g += step) {
+        const uint32_t gnext = g + step;
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];
         const uint32_t b = g - ps.first[k];
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-        prefetch_batch(ps, g + step, lane, nxt);
+        prefetch_batch(ps, gnext, lane, nxt);
         int32_t var_num;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)p.nblk, var_num, mlo,
@@ -562,7 +572,7 @@ static hipError_t launch_v3(const PlaneSet &ps, const DevTables *dev, unsigned l
     static const int per_cu = resident_per_cu(fdct8_quant_v3<A, V, S>, kFThreads);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_V3_GRID_MULT);
     hipLaunchKernelGGL((fdct8_quant_v3<A, V, S>), dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps, dev, fb);
     return hipGetLastError();
 }
@@ -698,7 +708,7 @@ hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipSt
         hipLaunchKernelGGL(fdct8_movement_v2, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps);
     } else {
         static const int per_cu = resident_per_cu(fdct8_movement, kFThreads);
-        const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_v3
+        const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_V3_GRID_MULT);  // the same grid as launch_v3
         hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps, dev);
     }
     return hipGetLastError();

@@ -25,6 +25,10 @@
 #include "fdct8_core.h"
 #include "pair_core.h"
 
+#ifndef DCTQ_RT_GRID_MULT
+#define DCTQ_RT_GRID_MULT DCTQ_GRID_MULT  // grid multiplier of this file's streaming kernels (dctq_internal.h)
+#endif
+
 namespace dctq {
 
 #ifndef DCTQ_RT_EARLY_PREFETCH
@@ -194,7 +198,7 @@ static hipError_t launch_rt(const RoundTripSet &rt, const DevTables *dev, unsign
     static const int per_cu = resident_per_cu(roundtrip8<A, V, S>, kThreads);
     const uint32_t nbatch = rt.ps.first[rt.ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_RT_GRID_MULT);
     hipLaunchKernelGGL((roundtrip8<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt, dev, fb);
     return hipGetLastError();
 }
@@ -273,7 +277,7 @@ hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream,
     static const int per_cu = resident_per_cu(roundtrip_movement, kThreads);
     const uint32_t nbatch = rt.ps.first[rt.ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_rt
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_RT_GRID_MULT);  // the same grid as launch_rt
     hipLaunchKernelGGL(roundtrip_movement, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt);
     return hipGetLastError();
 }

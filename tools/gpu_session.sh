@@ -51,6 +51,13 @@ for step in "$@"; do
     move5a) run move5a 180 tools/ubench/move5 12 3 ;;
     testnew) run pytest_new 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "stash or dist_legs or gpus2 or bench_json" ;;
     move5b) run move5b 180 tools/ubench/move5 12 3 ;;
+    abg) run abg 500 python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g12.so tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement ;;
+    abgb) run abgb 500 python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g12.so tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement ;;
+    abgx) run abgx 500 bash -c "python tools/lib_ab.py --rounds 6 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 6 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 6 --b2b 3 --kind const default tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so" ;;
+    auxab) run auxab 400 python tools/aux_ab.py ;;
+    rtab) run rtab 400 python tools/rt_bench.py 64 ;;
+    abv3) run abv3 400 python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_tabov.so tools/ubench/libvar_dyn1.so tools/ubench/libvar_dyn2.so tools/ubench/libvar_grid4.so tools/ubench/libvar_grid16.so movement ;;
+    abv3b) run abv3b 400 python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_tabov.so tools/ubench/libvar_dyn1.so tools/ubench/libvar_dyn2.so tools/ubench/libvar_grid4.so tools/ubench/libvar_grid16.so movement ;;
     phase) run phase 120 tools/ubench/hbm_phase 8 ;;
     planes) run planes 300 python tools/plane_bench.py ;;
     legacy) run legacy 120 host/legacy_latency ;;

@@ -89,9 +89,18 @@ __device__ __forceinline__ void pin(In<LOAD> &in) {
     }
 }
 
-template <int LOAD, int STAGE, int NB>
+__device__ double g_tab[128];  // stands in for the plan's exact tables (fdct8_quant_v3's LDS copy)
+
+// TAB 1: every workgroup starts as fdct8_quant_v3 does -- 1 KiB of tables from
+// global memory into LDS, then __syncthreads -- before its first batch's loads
+template <int LOAD, int STAGE, int NB, int TAB = 0>
 __global__ __launch_bounds__(256) void k_mv(Geo g, char *coef) {
     __shared__ uint4 st[(STAGE ? NB * 256 * 136 / 16 : 1) + 96];  // + the product's 1.5 KiB of tables/scratch
+    if (TAB) {
+        double *t = reinterpret_cast<double *>(st + (STAGE ? NB * 256 * 136 / 16 : 1));
+        for (int i = threadIdx.x; i < 128; i += blockDim.x) t[i] = g_tab[i];
+        __syncthreads();
+    }
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t step = gridDim.x * 4;
     uint32_t it = blockIdx.x * 4 + wv;  // iteration unit: NB consecutive batches
@@ -167,6 +176,62 @@ __global__ __launch_bounds__(256) void k_mv(Geo g, char *coef) {
     }
 }
 
+// Dynamic batch assignment (round 4): a persistent grid whose waves take the next
+// 64-block batch from a device counter (one vector atomic per batch, issued one
+// batch ahead so its latency hides behind the current batch), the rest as the
+// rows8 staged case.  The counters reset themselves: the last wave to finish
+// (the `fin` counter) zeroes both, so back-to-back launches need no memset.
+__global__ __launch_bounds__(256) void k_dyn(Geo g, char *coef, uint32_t *ctr) {
+    __shared__ uint4 st[256 * 136 / 16 + 96];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t n = g.nbatch;
+    auto grab = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    uint32_t cur = grab();
+    uint32_t nx = grab();
+    In<1> nxt;
+    if (cur < n) load_batch<1>(g, cur, lane, nxt);
+    pin<1>(nxt);
+    char *ws = reinterpret_cast<char *>(st) + wv * 8704;
+    while (cur < n) {
+        In<1> c = nxt;
+        const uint32_t nn = grab();  // the batch after next: its latency hides behind this batch
+        if (nx < n) load_batch<1>(g, nx, lane, nxt);
+        uint2 *mine = reinterpret_cast<uint2 *>(ws + lane * 136);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            mine[2 * k] = c.r[k];
+            mine[2 * k + 1] = make_uint2(c.r[k].y, c.r[k].x);
+        }
+        pin<1>(nxt);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        u4v val[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int m = k * 64 + lane, bl = m >> 3;
+            const uint2 *s2 = reinterpret_cast<const uint2 *>(ws + bl * 136 + (m & 7) * 16);
+            val[k] = u4v{s2[0].x, s2[0].y, s2[1].x, s2[1].y};
+        }
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(coef + (size_t)cur * 8192, 0, 8192, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rc, lane * 16, k * 1024, 2);
+        cur = nx;
+        nx = nn;
+    }
+    if (lane == 0) {
+        const uint32_t waves = gridDim.x * 4;
+        if (__hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == waves - 1) {
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __global__ void k_fill(uint32_t *p, size_t n, uint32_t seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull + seed;
@@ -213,16 +278,14 @@ int main(int argc, char **argv) {
         snprintf(buf, sizeof buf, "%s x%d (%d WG/CU res)", nm, mult, per);
         items.push_back({buf, [=] { hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, g, dst); }});
     };
-    for (int m : {1, 2, 8}) {
-        add("flat16 direct NB1", k_mv<0, 0, 1>, m);
+    // round 4, second call: the grid multiplier past x8 (the dynamic counter of k_dyn ran at 12 % of 8 TB/s:
+    // one address takes ~80 M atomics/s, profiles/r04/move5_grid.log -- dropped from the list)
+    for (int m : {4, 8, 12, 16, 24, 32, 48}) {
         add("flat16 staged NB1", k_mv<0, 1, 1>, m);
         add("rows8  staged NB1", k_mv<1, 1, 1>, m);
     }
-    for (int m : {1, 8}) {
-        add("flat16 direct NB2", k_mv<0, 0, 2>, m);
-        add("rows8  staged NB2", k_mv<1, 1, 2>, m);
-        add("flat16 direct NB4", k_mv<0, 0, 4>, m);
-    }
+    add("flat16 direct NB4", k_mv<0, 0, 4>, 1);
+    add("flat16 direct NB1", k_mv<0, 0, 1>, 1);
     for (int w = 0; w < 300; ++w) items[w % items.size()].fn();  // clock pre-warm
     CHECK(hipDeviceSynchronize());
     std::vector<std::vector<float>> us(items.size());
@@ -244,8 +307,8 @@ int main(int argc, char **argv) {
         std::vector<float> v = us[i];
         std::sort(v.begin(), v.end());
         const float med = v[v.size() / 2];
-        printf("%-40s median %7.1f us %5.1f %% | min %7.1f\n", items[i].name.c_str(), med, bytes / med / 1e6 / 80.0,
-               v[0]);
+        printf("%-40s median %7.1f us %5.1f %% of 8 TB/s | min %7.1f\n", items[i].name.c_str(), med,
+               bytes / (med * 1e-6) / 8e12 * 100.0, v[0]);
     }
     return 0;
 }
