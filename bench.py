@@ -726,8 +726,10 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
                     stage, 1 KiB stores), no math;
       movement_v2 : dctq_diag_movement_v2_planes -- the same for fdct8_quant_v2 (the
                     tie-heavy plans' queue kernel), an extra named ceiling;
-      flat_1to2_* : dctq_diag_stream 0/1 -- the same byte counts as a flat stream
-                    (16 B per lane, 1 KiB per instruction), nt / default stores,
+      flat_1to2_* : dctq_diag_stream 0/1/6/7 -- the same byte counts as a flat stream
+                    (16 B per lane, 1 KiB per instruction), nt / default stores, on the
+                    resident grid and on 16x / 32x grids (_x16, _x32: the grid the
+                    forward runs, and twice it),
                     reading THE SAME PIXEL BYTES (the luma and chroma stacks back to
                     back): HBM moves constant data faster than random data (up to
                     9 %), so a ceiling over a constant buffer is not a
@@ -768,6 +770,8 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
         "movement_v3": (lambda: dplan.diag_movement_planes(pls, outs), nblk * BYTES_PER_BLOCK),
         "movement_v2": (lambda: dplan.diag_movement_planes(pls, outs, shape=2), nblk * BYTES_PER_BLOCK),
         "flat_1to2_nt_nt": (lambda: diag_stream(0), nflat * BYTES_PER_BLOCK),
+        "flat_1to2_nt_nt_x16": (lambda: diag_stream(6), nflat * BYTES_PER_BLOCK),
+        "flat_1to2_nt_nt_x32": (lambda: diag_stream(7), nflat * BYTES_PER_BLOCK),
         "flat_1to2_nt_nt_const": (lambda: diag_stream(0, buf=src7), nflat * BYTES_PER_BLOCK),
         "flat_1to2_nt_plain": (lambda: diag_stream(1), nflat * BYTES_PER_BLOCK),
         "read_only": (lambda: diag_stream(2), nflat * 64),
@@ -790,7 +794,8 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
                 times[k].append(e0.elapsed_time(e1) * 1e-3 / b2b)
     med = {k: statistics.median(v) for k, v in times.items()}
     frac = {k: cases[k][1] / med[k] / 1e9 / HBM_PEAK_GBS for k in cases}
-    best = max(("movement_v3", "flat_1to2_nt_nt", "flat_1to2_nt_plain"), key=lambda k: frac[k])
+    best = max(("movement_v3", "flat_1to2_nt_nt", "flat_1to2_nt_nt_x16", "flat_1to2_nt_nt_x32", "flat_1to2_nt_plain"),
+               key=lambda k: frac[k])
     del src, src7, dst
     return {"pattern": best, "achieved": frac[best] * HBM_PEAK_GBS, "frac": frac[best],
             "forward_frac": frac["forward"], "forward_over_ceiling": frac["forward"] / frac[best],

@@ -51,7 +51,9 @@ int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes
  *   kind 3: write-only stream of blocks * 128 bytes of dst (default policy);
  *   kind 4: the same with non-temporal stores;
  *   kind 5: the round trip's mix, flat: 64 B read : 128 + 256 B written per
- *           block (per wave 4 x 1 KiB loads, 24 x 1 KiB nt stores), persistent.
+ *           block (per wave 4 x 1 KiB loads, 24 x 1 KiB nt stores), persistent;
+ *   kind 6, 7: kind 0 on a grid of 16 x / 32 x the resident one (the forward's
+ *           grid and twice it), capped at one 64-block batch per wave.
  * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kind 5: blocks * 384),
  * both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);

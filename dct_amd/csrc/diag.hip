@@ -164,7 +164,15 @@ int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, voi
         break;
     }
     case 5: hipLaunchKernelGGL(stream124, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
-    default: return fail(DCTQ_EINVAL, "kind must be 0..5");
+    case 6:
+    case 7: {
+        // kind 0 on a 16x / 32x grid (round 4: the forward's grid; the movement ubench's best for the flat
+        // stream too, profiles/r04/forward_grid_sweep.log), capped at one batch per wave
+        const unsigned want = (nb + 3) / 4, g = (unsigned)grid * (kind == 6 ? 16u : 32u);
+        hipLaunchKernelGGL(stream12<2>, dim3(g < want ? g : want), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb);
+        break;
+    }
+    default: return fail(DCTQ_EINVAL, "kind must be 0..7");
     }
     HIPCHK(hipGetLastError(), "diag stream launch");
     return DCTQ_OK;

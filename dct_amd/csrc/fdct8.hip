@@ -23,6 +23,10 @@
 // rounded the same way the reference rounds them.
 #include "fdct8_core.h"
 
+#ifndef DCTQ_V2_GRID_MULT
+#define DCTQ_V2_GRID_MULT DCTQ_GRID_MULT  // fdct8_quant_v2's grid (its stash is sized to it: 8 KiB per wave)
+#endif
+
 namespace dctq {
 
 // Reference-order fp64 recomputation of ONE quantized coefficient c = 8i + j:
@@ -478,7 +482,7 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
     static const int per_cu = resident_per_cu(fdct8_quant_v2<A, V, S>, kFThreads);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_V2_GRID_MULT);
     const uint32_t grid = want < cap ? want : cap;
     // the stash is sized to THIS grid (every workgroup owns its waves' slots) and
     // handed out by the caller per (device, stream): launches on one stream are
@@ -511,6 +515,9 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 // (v3 resolves ties in place) the grid costs nothing but workgroup starts; round 2's x16 regression
 // was the v2 queue kernel's.
 #define DCTQ_V3_GRID_MULT 16
+#endif
+#ifndef DCTQ_TIE_HEAVY_V3
+#define DCTQ_TIE_HEAVY_V3 0  // A/B: tie-heavy plans (DC divisor 1, q >= 97) on v3 too
 #endif
 #ifndef DCTQ_FWD_INPLACE
 #define DCTQ_FWD_INPLACE 1  // the product dispatch picks v3 (in-place ties) at every size unless the plan is tie-heavy
@@ -597,7 +604,7 @@ int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy
     // the resident grid (16 waves per CU: 4 per SIMD, VGPR-bound) has at most one
     // batch, where v2's end-of-kernel drain would be the whole tail
     const bool single = nbatch <= (uint32_t)(num_cus * 16);
-    return single || (DCTQ_FWD_INPLACE && !tie_heavy) ? 3 : 2;
+    return single || (DCTQ_FWD_INPLACE && (!tie_heavy || DCTQ_TIE_HEAVY_V3)) ? 3 : 2;
 }
 
 // ============================================================================
@@ -613,11 +620,20 @@ int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy
 //                        per lane and its stage read-back;
 //  fdct8_movement_v2  -- fdct8_quant_v2 (the tie-heavy plans' queue kernel): its
 //                        queue arrays and first-batch load_rows.
+#ifndef DCTQ_MV3_TAB
+#define DCTQ_MV3_TAB 1  // A/B: the workgroup-start table copy of fdct8_quant_v3
+#endif
+#ifndef DCTQ_MV3_SLEEP
+#define DCTQ_MV3_SLEEP 0  // A/B: s_sleep between the stage writes and the prefetch wait (64 clk units)
+#endif
+#ifndef DCTQ_MV3_B64
+#define DCTQ_MV3_B64 0  // A/B: b64 stage writes instead of fdct8_compute's 32 b32
+#endif
 __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, const DevTables *__restrict__ dev) {
     __shared__ uint4 stage[kFThreads * kPitch2 / 16];
     __shared__ ExactTables tab;
     __shared__ uint16_t scr[kFWaves * 64];
-    load_exact_tables(&tab, dev);
+    if (DCTQ_MV3_TAB) load_exact_tables(&tab, dev);
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (ps.n < 0) scr[threadIdx.x] = (uint16_t)tab.dct[lane];  // keep the footprint allocated
     const uint32_t nbatch = ps.first[ps.n];
@@ -637,10 +653,20 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, cons
         prefetch_batch(ps, g + step, lane, nxt);
         // fdct8_compute's stage writes: dword i*4 + cp of the lane's 136-B slot
         uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
+        if (DCTQ_MV3_B64) {  // A/B: 16 b64 writes (fdct8_movement_v2's)
+            uint2 *mine = reinterpret_cast<uint2 *>(st32);
 #pragma unroll
-        for (int cp = 0; cp < 4; ++cp)
+            for (int r = 0; r < 8; ++r) {
+                mine[2 * r] = cur[r];
+                mine[2 * r + 1] = make_uint2(cur[r].y, cur[r].x);
+            }
+        } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) st32[i * 4 + cp] = cp & 1 ? cur[i].y : cur[i].x ^ (uint32_t)cp;
+            for (int cp = 0; cp < 4; ++cp)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) st32[i * 4 + cp] = cp & 1 ? cur[i].y : cur[i].x ^ (uint32_t)cp;
+        }
+        if (DCTQ_MV3_SLEEP) __builtin_amdgcn_s_sleep(DCTQ_MV3_SLEEP);  // A/B: the arithmetic's latency slack
         asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                      "+v"(nxt[6]), "+v"(nxt[7])::"memory");
         wave_sync();
@@ -704,7 +730,7 @@ hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipSt
     const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
     if (shape == 2) {
         static const int per_cu = resident_per_cu(fdct8_movement_v2, kFThreads);
-        const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_GRID_MULT);  // the same grid as launch_v2
+        const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_V2_GRID_MULT);  // the same grid as launch_v2
         hipLaunchKernelGGL(fdct8_movement_v2, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps);
     } else {
         static const int per_cu = resident_per_cu(fdct8_movement, kFThreads);

@@ -54,6 +54,9 @@ for step in "$@"; do
     abg) run abg 500 python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g12.so tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement ;;
     abgb) run abgb 500 python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g12.so tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement ;;
     abgx) run abgx 500 bash -c "python tools/lib_ab.py --rounds 6 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 6 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 6 --b2b 3 --kind const default tools/ubench/libvar_g16.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so" ;;
+    abmv) run abmv 500 python tools/lib_ab.py --rounds 10 --b2b 3 default movement movement:tools/ubench/libvar_mv8.so movement:tools/ubench/libvar_mvnotab.so movement:tools/ubench/libvar_mvb64.so movement:tools/ubench/libvar_mvb64notab.so ;;
+    abmvs) run abmvs 500 python tools/lib_ab.py --rounds 10 --b2b 3 default movement movement:tools/ubench/libvar_mvs16.so movement:tools/ubench/libvar_mvs48.so movement:tools/ubench/libvar_mvs96.so ;;
+    abth) run abth 600 bash -c "python tools/lib_ab.py --rounds 6 --b2b 3 --quality 100 default tools/ubench/libvar_th3.so tools/ubench/libvar_v2g16.so movement && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 99 --adaptive 1 default tools/ubench/libvar_th3.so tools/ubench/libvar_v2g16.so && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 97 default tools/ubench/libvar_th3.so tools/ubench/libvar_v2g16.so && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 100 --kind smooth default tools/ubench/libvar_th3.so tools/ubench/libvar_v2g16.so && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 100 --kind extreme default tools/ubench/libvar_th3.so tools/ubench/libvar_v2g16.so" ;;
     auxab) run auxab 400 python tools/aux_ab.py ;;
     rtab) run rtab 400 python tools/rt_bench.py 64 ;;
     abv3) run abv3 400 python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_tabov.so tools/ubench/libvar_dyn1.so tools/ubench/libvar_dyn2.so tools/ubench/libvar_grid4.so tools/ubench/libvar_grid16.so movement ;;
