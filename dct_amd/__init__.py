@@ -65,6 +65,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
             "dctq_diag_plan_set_num_cus": ([vp, i], i),
             "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_movement_v2_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
+            "dctq_diag_movement_grid_planes": ([vp, C.POINTER(_Plane), i, vp, i, vp], i),
             "dctq_diag_rt_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_diag_stream": ([i, vp, vp, ll, vp], i),
             "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
@@ -232,7 +233,7 @@ class Plan:
                                                _stream_ptr(stream)))
         return outs
 
-    def diag_movement_planes(self, planes, outs, stream=None, shape: int = 3):
+    def diag_movement_planes(self, planes, outs, stream=None, shape: int = 3, grid_mult: int = 0):
         """DIAGNOSTIC: the bytes forward_quant_planes moves, with no arithmetic (outs receive
         pixel bytes, not coefficients) -- the memory ceiling of that access pattern."""
         n = len(planes)
@@ -241,6 +242,10 @@ class Plan:
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         if self._L is not _diag:
             raise DctqError("diag_movement_planes needs a plan of the diagnostic library (Plan(..., diagnostic=True))")
+        if grid_mult:
+            self._chk(self._L.dctq_diag_movement_grid_planes(self._h, descs, n, C.cast(cp, C.c_void_p), grid_mult,
+                                                             _stream_ptr(stream)))
+            return outs
         fn = self._L.dctq_diag_movement_planes if shape == 3 else self._L.dctq_diag_movement_v2_planes
         self._chk(fn(self._h, descs, n, C.cast(cp, C.c_void_p), _stream_ptr(stream)))
         return outs

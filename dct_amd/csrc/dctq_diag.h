@@ -32,6 +32,10 @@ int dctq_diag_plan_set_num_cus(dctq_plan *plan, int num_cus);
  * access pattern. */
 int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               void *stream);
+/* The same on a grid of grid_mult (1..64) x the resident workgroups instead of the
+ * product kernel's (bench.py: the pattern's ceiling at the round-3 grid, x8). */
+int dctq_diag_movement_grid_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                   int grid_mult, void *stream);
 /* The same in the access pattern of fdct8_quant_v2 (the tie-heavy plans' queue
  * kernel: its queue arrays in LDS, its first-batch loads). */
 int dctq_diag_movement_v2_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,

@@ -136,7 +136,9 @@ int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy
 size_t fdct8_ring_bytes(int workgroups);
 // diagnostic: the forward's data movement without arithmetic (fdct8.hip): shape 3 =
 // fdct8_quant_v3's (the product kernel), 2 = fdct8_quant_v2's (the tie-heavy plans' queue kernel)
-hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape);
+// shape 3: fdct8_movement, 2: fdct8_movement_v2; grid_mult 0 = the product kernel's grid
+hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape,
+                                 int grid_mult = 0);
 hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
                             hipStream_t stream, int num_cus);
 // diagnostic: roundtrip8's data movement without arithmetic (roundtrip.hip)

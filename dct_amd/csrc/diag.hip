@@ -112,6 +112,18 @@ int dctq_diag_movement_planes(const dctq_plan *plan, const dctq_plane *planes, i
     return DCTQ_OK;
 }
 
+int dctq_diag_movement_grid_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                   int grid_mult, void *stream) {
+    DCTQ_ENTRY;
+    if (int rc = dctq::check_plan(plan)) return rc;
+    if (grid_mult < 1 || grid_mult > 64) return dctq::fail(DCTQ_EINVAL, "grid_mult must be 1..64");
+    dctq::PlaneSet ps;
+    if (int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &ps)) return rc;
+    HIPCHK(dctq::launch_fdct8_movement(ps, plan->dev, (hipStream_t)stream, plan->num_cus, 3, grid_mult),
+           "fdct8_movement launch");
+    return DCTQ_OK;
+}
+
 int dctq_diag_movement_v2_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                                  void *stream) {
     DCTQ_ENTRY;

@@ -519,6 +519,9 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 #ifndef DCTQ_TIE_HEAVY_V3
 #define DCTQ_TIE_HEAVY_V3 0  // A/B: tie-heavy plans (DC divisor 1, q >= 97) on v3 too
 #endif
+#ifndef DCTQ_V3_LATE_FENCE
+#define DCTQ_V3_LATE_FENCE 0
+#endif
 #ifndef DCTQ_FWD_INPLACE
 #define DCTQ_FWD_INPLACE 1  // the product dispatch picks v3 (in-place ties) at every size unless the plan is tie-heavy
 #endif
@@ -552,9 +555,13 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)p.nblk, var_num, mlo,
                                            mhi);
         // the prefetch wait (retires the previous batch's stores too), then LDS reads
-        asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
-                     "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+        if (!DCTQ_V3_LATE_FENCE)
+            asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                         "+v"(nxt[6]), "+v"(nxt[7])::"memory");
         resolved += resolve_ties_compact<ADAPTIVE, DCTQ_V3_GROUP8>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+        if (DCTQ_V3_LATE_FENCE)  // A/B: the tie pass while the prefetch is in flight
+            asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                         "+v"(nxt[6]), "+v"(nxt[7])::"memory");
         wave_sync();
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
@@ -725,7 +732,8 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement_v2(PlaneSet ps) {
     }
 }
 
-hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape) {
+hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape,
+                                 int grid_mult) {
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t want = (nbatch + kFWaves - 1) / kFWaves;
     if (shape == 2) {
@@ -734,7 +742,7 @@ hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipSt
         hipLaunchKernelGGL(fdct8_movement_v2, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps);
     } else {
         static const int per_cu = resident_per_cu(fdct8_movement, kFThreads);
-        const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_V3_GRID_MULT);  // the same grid as launch_v3
+        const uint32_t cap = (uint32_t)(num_cus * per_cu * (grid_mult > 0 ? grid_mult : DCTQ_V3_GRID_MULT));  // launch_v3's
         hipLaunchKernelGGL(fdct8_movement, dim3(want < cap ? want : cap), dim3(kFThreads), 0, stream, ps, dev);
     }
     return hipGetLastError();

@@ -275,6 +275,26 @@ __device__ __forceinline__ void flat_dc_fix(const DevTables *__restrict__ dev, c
     }
 }
 
+// temp[k][j] = sum_l x[k][l] D^T[l][j], l ascending from 0.0 (src/dct.c:57-64), x = px - 128.
+// DCTQ_EXACT_NOZERO starts the sum at the first product instead of 0.0 + it (and
+// the callers start `out` at its first term): 0.0 + p == p for every p except
+// p == -0.0, so the sums differ at most in the sign of a zero, which neither a
+// later nonzero term nor round() / the int conversion can see -- the int16
+// result is the reference's.  9 fp64 adds fewer per evaluation.
+#ifndef DCTQ_EXACT_NOZERO
+#define DCTQ_EXACT_NOZERO 0
+#endif
+__device__ __forceinline__ double row_sum(uint32_t wx, uint32_t wy, const double *dj) {
+    double t = 0.0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const uint32_t w = l < 4 ? wx : wy;
+        const double p = ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
+        t = l == 0 && DCTQ_EXACT_NOZERO ? p : t + p;
+    }
+    return t;
+}
+
 // The arithmetic of exact_quant() (fdct8.hip) on a block held in registers plus,
 // for adaptive plans, the block's exact variance and adjusted divisor
 // (src/quantization.c:153-211):
@@ -308,13 +328,8 @@ __device__ __forceinline__ int exact_from_rows(const uint2 (&rows)[8], int c, co
     double out = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        double t = 0.0;
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            const uint32_t w = l < 4 ? rows[k].x : rows[k].y;
-            t += ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
-        }
-        out += di[k] * t;
+        const double t = row_sum(rows[k].x, rows[k].y, dj);
+        out = k == 0 && DCTQ_EXACT_NOZERO ? di[0] * t : out + di[k] * t;
     }
     return (int)round(out / m);
 }
@@ -385,13 +400,8 @@ __device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c
     double out = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        double t = 0.0;
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            const uint32_t w = l < 4 ? rows[k].x : rows[k].y;
-            t += ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
-        }
-        out += di[k] * t;
+        const double t = row_sum(rows[k].x, rows[k].y, dj);
+        out = k == 0 && DCTQ_EXACT_NOZERO ? di[0] * t : out + di[k] * t;
     }
     return (int)round(out / m);
 }
@@ -412,7 +422,8 @@ __device__ __forceinline__ void group8_sum(uint64_t tb, const double *di, double
     if constexpr (Q < 8) {
         const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)tb, 0x18 | (Q << 5));
         const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(tb >> 32), 0x18 | (Q << 5));
-        out += di[Q] * __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        const double p = di[Q] * __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        out = Q == 0 && DCTQ_EXACT_NOZERO ? p : out + p;
         group8_sum<Q + 1>(tb, di, out);
     }
 }
@@ -441,12 +452,7 @@ __device__ __forceinline__ uint32_t exact_grouped8(const ExactTables *tab, const
     }
     const double *dj = tab->dct + (c & 7) * 8;  // D^T[l][j]
     const double *di = tab->dct + (c >> 3) * 8;  // D[i][k]
-    double t = 0.0;
-#pragma unroll
-    for (int l = 0; l < 8; ++l) {
-        const uint32_t w = l < 4 ? rx : ry;
-        t += ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
-    }
+    const double t = row_sum(rx, ry, dj);
     const uint64_t tb = __builtin_bit_cast(uint64_t, t);
     double out = 0.0;
     group8_sum<0>(tb, di, out);

@@ -87,6 +87,9 @@ for step in "$@"; do
     ab234) run ab234 300 bash -c "python tools/ab_bench.py --variants 2,3,4 --rounds 12 && python tools/ab_bench.py --variants 2,3,4 --rounds 8 --kind smooth && python tools/ab_bench.py --variants 2,3,4 --rounds 6 --kind const" ;;
     ab) run ab 300 python tools/ab_bench.py --variants 1,2 ;;
     abk) run abk 300 bash -c "python tools/ab_bench.py --kind smooth && python tools/ab_bench.py --kind const && python tools/ab_bench.py --adaptive 1 && python tools/ab_bench.py --quality 90" ;;
+    stepov) run stepov 300 python tools/step_overhead.py ;;
+    abth2) run abth2 700 bash -c "python tools/lib_ab.py --rounds 6 --b2b 3 --quality 100 default tools/ubench/libvar_th3.so tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3lf.so tools/ubench/libvar_th3nz.so tools/ubench/libvar_th3all.so movement && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 100 --kind smooth default tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3all.so && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 99 --adaptive 1 default tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3all.so && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 97 default tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3all.so" ;;
+    abq50) run abq50 500 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_nz.so tools/ubench/libvar_lf.so movement && python tools/lib_ab.py --rounds 6 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_nz.so tools/ubench/libvar_lf.so && python tools/lib_ab.py --rounds 6 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_nz.so tools/ubench/libvar_lf.so" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
