@@ -34,7 +34,10 @@ __device__ __forceinline__ void fence_rows(uint2 (&nxt)[8]) {
 __device__ __forceinline__ uint32_t nz16e(uint32_t w) { return ((w & 0xFFFFu) != 0u) + ((w >> 16) != 0u); }
 
 #ifndef DCTQ_ENC_GROUP8
-#define DCTQ_ENC_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped8): -0.9 %
+#define DCTQ_ENC_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>): -0.9 %
+#endif
+#ifndef DCTQ_ENC_WIDE
+#define DCTQ_ENC_WIDE 0  // resolve_ties_compact WIDE: at this kernel's 128-VGPR bound the wide rounds spill (A/B knob)
 #endif
 
 template <bool ADAPTIVE>
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, false>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)nblk, vn, mlo, mhi);
         fence_rows(nxt);  // the prefetch wait: retires the previous batch's stores too
-        resolve_ties_compact<ADAPTIVE, DCTQ_ENC_GROUP8>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+        resolve_ties_compact<ADAPTIVE, DCTQ_ENC_GROUP8, DCTQ_ENC_WIDE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         wave_sync();
         u4v q[8];
         stage_chunks(stage, wv, lane, q);

@@ -505,7 +505,10 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 // 512x512 = 64 batches, 4K = 2 025) v2's end-of-kernel drain -- vmcnt(0), stash
 // loads, fp64, patch stores -- is the whole tail of the launch.
 #ifndef DCTQ_V3_GROUP8
-#define DCTQ_V3_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped8)
+#define DCTQ_V3_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>)
+#endif
+#ifndef DCTQ_V3_WIDE
+#define DCTQ_V3_WIDE 0  // resolve_ties_compact WIDE: at this kernel's 128-VGPR bound the wide rounds spill (A/B knob)
 #endif
 #ifndef DCTQ_V3_GRID_MULT
 // fdct8_quant_v3 launches 16 x its resident workgroups (round 4, profiles/r04/forward_grid_sweep.log,
@@ -525,14 +528,20 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 #ifndef DCTQ_FWD_INPLACE
 #define DCTQ_FWD_INPLACE 1  // the product dispatch picks v3 (in-place ties) at every size unless the plan is tie-heavy
 #endif
+#ifndef DCTQ_V3_WAVE_TAB
+#define DCTQ_V3_WAVE_TAB 0  // A/B: each wave its own exact-table copy, loaded with its first rows (no s_barrier)
+#endif
 template <bool ADAPTIVE, bool VAR, bool STATS>
 __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, const DevTables *__restrict__ dev,
                                                               unsigned long long *fallbacks) {
     __shared__ uint4 stage[kFThreads * kPitch2 / 16];
-    __shared__ ExactTables tab;
+    __shared__ ExactTables tabs[DCTQ_V3_WAVE_TAB ? kFWaves : 1];
     __shared__ uint16_t scr[kFWaves * 64];  // resolve_ties_compact's entries
-    load_exact_tables(&tab, dev);
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    ExactTables &tab = tabs[DCTQ_V3_WAVE_TAB ? wv : 0];
+    double tl[2];
+    if (DCTQ_V3_WAVE_TAB) wave_tables_load(dev, lane, tl);
+    else load_exact_tables(&tab, dev);
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kFWaves;
     uint32_t g = blockIdx.x * kFWaves + wv;
@@ -540,6 +549,10 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
     prefetch_batch(ps, g, lane, nxt);
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    if (DCTQ_V3_WAVE_TAB) {
+        wave_tables_store(&tab, lane, tl);
+        wave_sync();
+    }
     uint32_t resolved = 0;
     for (; g < nbatch; g += step) {
         const uint32_t gnext = g + step;
@@ -558,7 +571,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         if (!DCTQ_V3_LATE_FENCE)
             asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                          "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-        resolved += resolve_ties_compact<ADAPTIVE, DCTQ_V3_GROUP8>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+        resolved += resolve_ties_compact<ADAPTIVE, DCTQ_V3_GROUP8, DCTQ_V3_WIDE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (DCTQ_V3_LATE_FENCE)  // A/B: the tie pass while the prefetch is in flight
             asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                          "+v"(nxt[6]), "+v"(nxt[7])::"memory");
@@ -638,10 +651,13 @@ int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy
 #endif
 __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, const DevTables *__restrict__ dev) {
     __shared__ uint4 stage[kFThreads * kPitch2 / 16];
-    __shared__ ExactTables tab;
+    __shared__ ExactTables tabs[DCTQ_V3_WAVE_TAB ? kFWaves : 1];
     __shared__ uint16_t scr[kFWaves * 64];
-    if (DCTQ_MV3_TAB) load_exact_tables(&tab, dev);
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    ExactTables &tab = tabs[DCTQ_V3_WAVE_TAB ? wv : 0];
+    double tl[2];
+    if (DCTQ_V3_WAVE_TAB) wave_tables_load(dev, lane, tl);
+    else if (DCTQ_MV3_TAB) load_exact_tables(&tab, dev);
     if (ps.n < 0) scr[threadIdx.x] = (uint16_t)tab.dct[lane];  // keep the footprint allocated
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kFWaves;
@@ -650,6 +666,10 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, cons
     prefetch_batch(ps, g, lane, nxt);
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    if (DCTQ_V3_WAVE_TAB) {
+        wave_tables_store(&tab, lane, tl);
+        wave_sync();
+    }
     for (; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];

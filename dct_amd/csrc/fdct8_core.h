@@ -282,7 +282,7 @@ __device__ __forceinline__ void flat_dc_fix(const DevTables *__restrict__ dev, c
 // later nonzero term nor round() / the int conversion can see -- the int16
 // result is the reference's.  9 fp64 adds fewer per evaluation.
 #ifndef DCTQ_EXACT_NOZERO
-#define DCTQ_EXACT_NOZERO 0
+#define DCTQ_EXACT_NOZERO 1
 #endif
 __device__ __forceinline__ double row_sum(uint32_t wx, uint32_t wy, const double *dj) {
     double t = 0.0;
@@ -372,6 +372,21 @@ __device__ __forceinline__ void load_exact_tables(ExactTables *t, const DevTable
     __syncthreads();
 }
 
+// A wave's own copy of the exact tables, without a workgroup barrier: each lane
+// requests entries lane and 64 + lane (D and Q) with the wave's first pixel rows
+// (wave_tables_load: their latency overlaps), and writes them to the wave's LDS copy
+// once those rows have arrived (wave_tables_store, then wave_sync).  The
+// workgroup-wide copy (load_exact_tables) is a global load, a vmcnt(0) and an
+// s_barrier in front of every workgroup's first prefetch.
+__device__ __forceinline__ void wave_tables_load(const DevTables *__restrict__ dev, int lane, double (&t)[2]) {
+    t[0] = dev->dct[lane];
+    t[1] = dev->quant[lane];
+}
+__device__ __forceinline__ void wave_tables_store(ExactTables *mine, int lane, const double (&t)[2]) {
+    mine->dct[lane] = t[0];
+    mine->quant[lane] = t[1];
+}
+
 // exact_from_rows() with the tables from LDS.
 template <bool ADAPTIVE>
 __device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c, const ExactTables *tab) {
@@ -406,60 +421,100 @@ __device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c
     return (int)round(out / m);
 }
 
-// exact_from_rows_lds() for e <= 8 entries of one pass, 8 lanes per entry
-// (lane = 8 * entry + k): lane k pulls row k of the entry's block from the
-// owning lane and sums it in the reference's order (temp[k][j], src/dct.c:57-66);
-// the group's 8 row sums are broadcast to every lane of the group (ds_swizzle)
-// and summed in row order (src/dct.c:67-74); the group's first lane stores
-// round(out / M) (src/quantization.c:124) and returns 1 (its entry resolved).  ~100 VALU per lane against ~290 for
-// one entry per lane: for passes with few entries (the fused Huffman kernel,
-// where most batches hold one or two).  Adaptive plans sum the block's variance
-// terms over the group (group8_add).
-// out += D[i][q] * (row q's sum, from lane 8 * group + q: ds_swizzle with
-// and_mask 0x18, or_mask q), q = Q .. 7 in order.
-template <int Q>
-__device__ __forceinline__ void group8_sum(uint64_t tb, const double *di, double &out) {
-    if constexpr (Q < 8) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)tb, 0x18 | (Q << 5));
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(tb >> 32), 0x18 | (Q << 5));
-        const double p = di[Q] * __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-        out = Q == 0 && DCTQ_EXACT_NOZERO ? p : out + p;
-        group8_sum<Q + 1>(tb, di, out);
-    }
-}
-
-// Sum of v over the lane's group of 8 (ds_swizzle xor 1, 2, 4 within 32 lanes).
-__device__ __forceinline__ uint32_t group8_add(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (1 << 10));
-    v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (2 << 10));
-    v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (4 << 10));
+// exact_from_rows_lds() for e <= 64 / G entries of one round, G = 8, 4 or 2 lanes
+// per entry (lane = G * entry + part): each lane pulls R = 8 / G rows of the entry's
+// block (rows part * R ..) from the owning lane and sums each in the reference's
+// order (temp[k][j], src/dct.c:57-66); the group's first lane holds rows 0 .. R - 1
+// and fetches the others' sums (ds_swizzle within the group), adding them in row
+// order (src/dct.c:67-74); it stores round(out / M) (src/quantization.c:124) and
+// returns 1 (its entry resolved).  Per round, against ~290 VALU for a pass of one
+// entry per lane: ~100 (G = 8), ~125 (G = 4), ~190 (G = 2), so a pass of e entries
+// takes the narrowest group that fits it in one round (resolve_ties_compact).
+// Adaptive plans sum the block's variance terms over the group (group_add).
+// Sum of v over the lane's group of G (ds_swizzle xor 1 .. G / 2 within 32 lanes).
+template <int G>
+__device__ __forceinline__ uint32_t group_add(uint32_t v) {
+    if constexpr (G >= 2) v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (1 << 10));
+    if constexpr (G >= 4) v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (2 << 10));
+    if constexpr (G >= 8) v += (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (4 << 10));
     return v;
 }
 
-template <bool ADAPTIVE>
-__device__ __forceinline__ uint32_t exact_grouped8(const ExactTables *tab, const uint2 (&cur)[8], int16_t *st16,
-                                                   const uint16_t *scr, int lane, uint32_t e) {
-    const int grp = lane >> 3, k = lane & 7;
+// out += D[i][q] * temp[q][j] for q = Q .. 7 in order: rows below R are the group
+// leader's own, row q >= R comes from lane (lane & ~(G - 1)) + q / R (ds_swizzle
+// bit mode: and_mask 0x1F & ~(G - 1), or_mask q / R).
+template <int G, int Q>
+__device__ __forceinline__ void group_sum(const double (&t)[8 / G], const double *di, double &out) {
+    if constexpr (Q < 8) {
+        constexpr int R = 8 / G;
+        double tq;
+        if constexpr (Q < R) {
+            tq = t[Q];
+        } else {
+            constexpr int pat = (0x1F & ~(G - 1)) | ((Q / R) << 5);
+            const uint64_t tb = __builtin_bit_cast(uint64_t, t[Q % R]);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)tb, pat);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_swizzle((int)(uint32_t)(tb >> 32), pat);
+            tq = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        }
+        const double p = di[Q] * tq;
+        out = Q == 0 && DCTQ_EXACT_NOZERO ? p : out + p;
+        group_sum<G, Q + 1>(t, di, out);
+    }
+}
+
+template <int G, bool ADAPTIVE>
+__device__ __forceinline__ uint32_t exact_grouped(const ExactTables *tab, const uint2 (&cur)[8], int16_t *st16,
+                                                  const uint16_t *scr, int lane, uint32_t e) {
+    constexpr int R = 8 / G;
+    const int grp = lane / G, part = lane % G;
     const uint32_t ent = (uint32_t)grp < e ? (uint32_t)scr[grp] : 0u;
     const int src = (int)(ent >> 6), c = (int)(ent & 63u);
-    uint32_t rx = 0, ry = 0;
+    uint32_t rx[R], ry[R];  // rows part * R + i of the entry's block
+#pragma unroll
+    for (int i = 0; i < R; ++i) rx[i] = ry[i] = 0u;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)cur[q].x);
         const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)cur[q].y);
-        rx = k == q ? x : rx;
-        ry = k == q ? y : ry;
+        rx[q % R] = part == q / R ? x : rx[q % R];
+        ry[q % R] = part == q / R ? y : ry[q % R];
     }
     const double *dj = tab->dct + (c & 7) * 8;  // D^T[l][j]
-    const double *di = tab->dct + (c >> 3) * 8;  // D[i][k]
-    const double t = row_sum(rx, ry, dj);
-    const uint64_t tb = __builtin_bit_cast(uint64_t, t);
+    double t[R];
+    if constexpr (R == 1) {
+        t[0] = row_sum(rx[0], ry[0], dj);
+    } else {
+        // the R sums side by side, l ascending in each (row_sum's order): one D^T[l][j]
+        // live at a time
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const double d = dj[l];
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const uint32_t w = l < 4 ? rx[i] : ry[i];
+                const double p = ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * d;
+                t[i] = l == 0 && DCTQ_EXACT_NOZERO ? p : (l == 0 ? 0.0 + p : t[i] + p);
+            }
+        }
+    }
+    // D[i][k] read only now: loaded with dj at the top (the compiler's choice) its 16
+    // VGPRs were live across the row sums and the wide groups spilled
+    int irow = (c >> 3) * 8;
+    asm volatile("" : "+v"(irow), "+v"(t[0]));
+    const double *di = tab->dct + irow;  // D[i][k]
     double out = 0.0;
-    group8_sum<0>(tb, di, out);
+    group_sum<G, 0>(t, di, out);
     double m = tab->quant[c];
     if (ADAPTIVE) {  // the block's exact variance from the group's rows (exact_from_rows_lds)
-        const uint32_t s1 = group8_add(__builtin_amdgcn_udot4(ry, 0x01010101u, __builtin_amdgcn_udot4(rx, 0x01010101u, 0u, false), false));
-        const uint32_t s2 = group8_add(__builtin_amdgcn_udot4(ry, ry, __builtin_amdgcn_udot4(rx, rx, 0u, false), false));
+        uint32_t s1 = 0u, s2 = 0u;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            s1 = __builtin_amdgcn_udot4(ry[i], 0x01010101u, __builtin_amdgcn_udot4(rx[i], 0x01010101u, s1, false), false);
+            s2 = __builtin_amdgcn_udot4(ry[i], ry[i], __builtin_amdgcn_udot4(rx[i], rx[i], s2, false), false);
+        }
+        s1 = group_add<G>(s1);
+        s2 = group_add<G>(s2);
         if (c != 0) {
             const int32_t sx = (int32_t)s1 - 8192;
             const int32_t sxx = (int32_t)s2 - 256 * (int32_t)s1 + 1048576;
@@ -467,7 +522,7 @@ __device__ __forceinline__ uint32_t exact_grouped8(const ExactTables *tab, const
             if (m < 1.0) m = 1.0;
         }
     }
-    if (k == 0 && (uint32_t)grp < e) {
+    if (part == 0 && (uint32_t)grp < e) {
         st16[src * (kPitch2 / 2) + c] = (int16_t)(int)round(out / m);
         return 1u;
     }
@@ -497,7 +552,10 @@ __device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict_
 #ifndef DCTQ_GROUP8_MAX
 #define DCTQ_GROUP8_MAX 8u  // GROUP8 passes with up to this many entries run in rounds of 8 lanes per entry
 #endif
-template <bool ADAPTIVE, bool GROUP8 = false>
+// WIDE (with GROUP8): bit 0 / bit 1 -- passes of 9..16 / 17..32 entries run as one round of
+// 4 / 2 lanes per entry (exact_grouped) instead of one entry per lane.  Per kernel: the
+// register-bound kernels (128 VGPRs at 4 waves/SIMD) spill with them.
+template <bool ADAPTIVE, bool GROUP8 = false, int WIDE = 0>
 __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab, const uint2 (&cur)[8], uint4 *stage,
                                                          uint16_t *scr, int lane, int wv, uint32_t &mlo,
                                                          uint32_t &mhi) {
@@ -520,7 +578,17 @@ __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab,
         if constexpr (GROUP8) {
             if (e <= DCTQ_GROUP8_MAX) {  // wave-uniform: rounds of 8 entries (~100 VALU each, against ~290 for a pass)
                 for (uint32_t e0 = 0; e0 < e; e0 += 8u)
-                    mine += exact_grouped8<ADAPTIVE>(tab, cur, st16, scr + e0, lane, e - e0 < 8u ? e - e0 : 8u);
+                    mine += exact_grouped<8, ADAPTIVE>(tab, cur, st16, scr + e0, lane, e - e0 < 8u ? e - e0 : 8u);
+                wave_sync();
+                continue;
+            }
+            if ((WIDE & 1) && e <= 16u) {  // one round of 4 lanes per entry (~125 VALU)
+                mine += exact_grouped<4, ADAPTIVE>(tab, cur, st16, scr, lane, e);
+                wave_sync();
+                continue;
+            }
+            if ((WIDE & 2) && e <= 32u) {  // one round of 2 lanes per entry (~190 VALU)
+                mine += exact_grouped<2, ADAPTIVE>(tab, cur, st16, scr, lane, e);
                 wave_sync();
                 continue;
             }

@@ -786,7 +786,13 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
 }
 
 #ifndef DCTQ_HP_GROUP8
-#define DCTQ_HP_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped8): -4.1 % uniform, -3.1 % smooth
+#define DCTQ_HP_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>): -4.1 % uniform, -3.1 % smooth
+#endif
+#ifndef DCTQ_HP_WIDE
+// passes of 9..32 entries in one round of 4 / 2 lanes per entry (resolve_ties_compact WIDE):
+// -2.7 % on extreme q10 (~10 entries per batch), uniform q50 unchanged (profiles/r04/wide_groups_ab.log);
+// no scratch at this kernel's 168-VGPR bound
+#define DCTQ_HP_WIDE 3
 #endif
 #ifndef DCTQ_HUF_MIN_WAVES
 #define DCTQ_HUF_MIN_WAVES 3
@@ -898,7 +904,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         mlo = mhi = 0;
 #endif
         if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0))
-            (void)resolve_ties_compact<ADAPTIVE, DCTQ_HP_GROUP8>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
+            (void)resolve_ties_compact<ADAPTIVE, DCTQ_HP_GROUP8, DCTQ_HP_WIDE>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
         wave_sync();
         prefetch_batch(ps, g + step, lane, cur);  // the rows are dead now; nothing past the last batch
         if (nb < 64) {  // blocks past the end are empty

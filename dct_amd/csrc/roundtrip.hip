@@ -38,7 +38,10 @@ namespace dctq {
 #define DCTQ_RT_OCC 4  // waves per SIMD (launch bound)
 #endif
 #ifndef DCTQ_RT_GROUP8
-#define DCTQ_RT_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped8): -4.9 % on the bench step
+#define DCTQ_RT_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>): -4.9 % on the bench step
+#endif
+#ifndef DCTQ_RT_WIDE
+#define DCTQ_RT_WIDE 0  // resolve_ties_compact WIDE: at this kernel's 128-VGPR bound the wide rounds spill (A/B knob)
 #endif
 
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
         retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
         const uint32_t ne =
-            resolve_ties_compact<ADAPTIVE, DCTQ_RT_GROUP8>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+            resolve_ties_compact<ADAPTIVE, DCTQ_RT_GROUP8, DCTQ_RT_WIDE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
         wave_sync();
 

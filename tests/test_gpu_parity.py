@@ -565,14 +565,15 @@ def _tie_count_plane(rng, counts):
 
 
 def test_grouped_tie_passes(T, dm):
-    """Tie passes of 0..12 entries per batch around the grouped path's bound (<= 8
-    entries: 8 lanes per entry, exact_grouped8; above: one entry per lane) in every
-    kernel that resolves ties in place -- the forward (v3; v2 forced beside it), the
-    fused round trip, the encoder and the fused Huffman sizes -- for both modes, with
-    the fallback counter counting every entry once."""
+    """Tie passes of 0..64 entries per batch around every grouped path's bound (<= 8
+    entries: 8 lanes per entry; 9..16 and 17..32 in the kernels with wide rounds, the
+    fused Huffman sizes: 4 and 2 lanes per entry; above: one entry per lane;
+    exact_grouped<G>) in every kernel that resolves ties in place -- the forward (v3;
+    v2 forced beside it), the fused round trip, the encoder and the fused Huffman
+    sizes -- for both modes, with the fallback counter counting every entry once."""
     import oracle as O
     rng = np.random.default_rng(77)
-    counts = [0, 1, 2, 3, 5, 7, 8, 9, 12, 8, 1, 16] * 2
+    counts = [0, 1, 2, 3, 5, 7, 8, 9, 12, 15, 16, 17, 20, 24, 31, 32, 33, 40, 48, 63, 64, 8, 1, 16] * 2
     px = _tie_count_plane(rng, counts)
     g = gpu_px(T, px)
     for ad in (0, 1):

@@ -90,6 +90,15 @@ for step in "$@"; do
     stepov) run stepov 300 python tools/step_overhead.py ;;
     abth2) run abth2 700 bash -c "python tools/lib_ab.py --rounds 6 --b2b 3 --quality 100 default tools/ubench/libvar_th3.so tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3lf.so tools/ubench/libvar_th3nz.so tools/ubench/libvar_th3all.so movement && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 100 --kind smooth default tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3all.so && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 99 --adaptive 1 default tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3all.so && python tools/lib_ab.py --rounds 6 --b2b 3 --quality 97 default tools/ubench/libvar_th3g8.so tools/ubench/libvar_th3all.so" ;;
     abq50) run abq50 500 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_nz.so tools/ubench/libvar_lf.so movement && python tools/lib_ab.py --rounds 6 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_nz.so tools/ubench/libvar_lf.so && python tools/lib_ab.py --rounds 6 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_nz.so tools/ubench/libvar_lf.so" ;;
+    abth3) run abth3 900 bash -c "python tools/lib_ab.py --rounds 12 --b2b 3 --quality 100 default tools/ubench/libvar_nz.so tools/ubench/libvar_th3nz.so tools/ubench/libvar_th3nzlf.so tools/ubench/libvar_th3all.so movement movement8 && python tools/lib_ab.py --rounds 12 --b2b 3 --quality 100 --kind smooth default tools/ubench/libvar_nz.so tools/ubench/libvar_th3nz.so tools/ubench/libvar_th3nzlf.so tools/ubench/libvar_th3all.so movement movement8 && python tools/lib_ab.py --rounds 12 --b2b 3 --quality 100 --kind extreme default tools/ubench/libvar_nz.so tools/ubench/libvar_th3nz.so tools/ubench/libvar_th3nzlf.so tools/ubench/libvar_th3all.so movement movement8 && python tools/lib_ab.py --rounds 12 --b2b 3 --quality 99 --adaptive 1 default tools/ubench/libvar_nz.so tools/ubench/libvar_th3nz.so tools/ubench/libvar_th3nzlf.so tools/ubench/libvar_th3all.so movement movement8 && python tools/lib_ab.py --rounds 12 --b2b 3 --quality 97 default tools/ubench/libvar_nz.so tools/ubench/libvar_th3nz.so tools/ubench/libvar_th3nzlf.so tools/ubench/libvar_th3all.so movement movement8" ;;
+    abgw1) run abgw1 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 --quality 100 default tools/ubench/libvar_ctl.so tools/ubench/libvar_pctl.so tools/ubench/libvar_pnz.so tools/ubench/libvar_pth3.so tools/ubench/libvar_pgw.so movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 --quality 100 --kind smooth default tools/ubench/libvar_ctl.so tools/ubench/libvar_pctl.so tools/ubench/libvar_pnz.so tools/ubench/libvar_pth3.so tools/ubench/libvar_pgw.so movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 --quality 99 --adaptive 1 default tools/ubench/libvar_ctl.so tools/ubench/libvar_pctl.so tools/ubench/libvar_pnz.so tools/ubench/libvar_pth3.so tools/ubench/libvar_pgw.so movement8" ;;
+    abgw2) run abgw2 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 --quality 50 default tools/ubench/libvar_pctl.so tools/ubench/libvar_pnz.so tools/ubench/libvar_pgw.so movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 --quality 10 --kind extreme default tools/ubench/libvar_pctl.so tools/ubench/libvar_pnz.so tools/ubench/libvar_pgw.so movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 --quality 97 default tools/ubench/libvar_pctl.so tools/ubench/libvar_pnz.so tools/ubench/libvar_pgw.so movement8" ;;
+    rtgw) run rtgw 400 bash -c "python tools/rt_bench.py 64 && python tools/rt_bench.py 64 --kind=extreme --q=10" ;;
+    hpgw) run hpgw 400 bash -c "python tools/huf_pixels_ab.py uniform 50 && python tools/huf_pixels_ab.py extreme 10" ;;
+    order) run order 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 --quality 100 tools/ubench/libvar_pctl.so default tools/ubench/libvar_copy.so tools/ubench/libvar_pnz.so && python tools/lib_ab.py --rounds 10 --b2b 3 --quality 100 tools/ubench/libvar_copy.so tools/ubench/libvar_pctl.so default && python tools/lib_ab.py --rounds 10 --b2b 3 --quality 100 default tools/ubench/libvar_copy.so tools/ubench/libvar_pctl.so && python tools/lib_ab.py --rounds 10 --b2b 3 --quality 50 tools/ubench/libvar_copy.so default tools/ubench/libvar_pctl.so" ;;
+    hpw) run hpw 500 bash -c "python tools/huf_pixels_ab.py uniform 50 && python tools/huf_pixels_ab.py extreme 10 && python tools/huf_pixels_ab.py smooth 90 && python tools/huf_pixels_ab.py uniform 99" ;;
+    abnz) run abnz 500 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_nz0.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 default tools/ubench/libvar_nz0.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_nz0.so" ;;
+    abwt) run abwt 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so movement movement8 movement:tools/ubench/libvar_mwt.so movement:tools/ubench/libvar_mwt32.so && python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so movement movement8 movement:tools/ubench/libvar_mwt.so movement:tools/ubench/libvar_mwt32.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

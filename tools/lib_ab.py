@@ -50,8 +50,10 @@ stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 builds = {}
 for path in args.libs:
-    mv = path == "movement" or path.startswith("movement:")
-    p = {"default": dct_amd.LIB_PATH, "movement": dct_amd.DIAG_PATH}.get(path) or os.path.abspath(path.split(":", 1)[-1])
+    mv8 = path == "movement8"  # the movement diagnostic on the x8 grid (dctq_diag_movement_grid_planes)
+    mv = mv8 or path == "movement" or path.startswith("movement:")
+    p = {"default": dct_amd.LIB_PATH, "movement": dct_amd.DIAG_PATH, "movement8": dct_amd.DIAG_PATH}.get(path) or \
+        os.path.abspath(path.split(":", 1)[-1])
     L = C.CDLL(p)
     L.dctq_plan_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.dctq_forward_quant_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p, C.c_void_p,
@@ -61,11 +63,16 @@ for path in args.libs:
     if mv:
         L.dctq_diag_movement_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p,
                                                 C.c_void_p]
-    builds[("movement:" if mv else "") + os.path.basename(p)] = (L, h)
+    if mv8:
+        L.dctq_diag_movement_grid_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p,
+                                                     C.c_int, C.c_void_p]
+    builds[("movement8:" if mv8 else "movement:" if mv else "") + os.path.basename(p)] = (L, h)
 
 
 def launch(L, h, name=""):
-    if name.startswith("movement:"):
+    if name.startswith("movement8:"):
+        rc = L.dctq_diag_movement_grid_planes(h, descs, len(planes), C.cast(optr, C.c_void_p), 8, stream)
+    elif name.startswith("movement:"):
         rc = L.dctq_diag_movement_planes(h, descs, len(planes), C.cast(optr, C.c_void_p), stream)
     else:
         rc = L.dctq_forward_quant_planes(h, descs, len(planes), C.cast(optr, C.c_void_p), None, stream)
@@ -74,7 +81,7 @@ def launch(L, h, name=""):
 
 ref = None
 for name, (L, h) in builds.items():
-    if name.startswith("movement:"):
+    if name.startswith("movement"):
         continue
     for o in outs:
         o.zero_()
