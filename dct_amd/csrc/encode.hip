@@ -58,12 +58,15 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
     fence_rows(nxt);
     for (; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
-        const uint32_t b = g - ps.first[k];
+        const uint32_t b = g - first_of(ps, k);
         const int nblk = ps.pl[k].nblk;
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         prefetch_batch(ps, g + step, lane, nxt);
+        const BatchOut out = batch_out(ps, k, b);  // resolved before the fence (fdct8_core.h)
+        uint32_t *off = offsets + es.blk_first[k] + (size_t)b * 64;
+        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(off));
         int32_t vn;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, false>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)nblk, vn, mlo, mhi);
@@ -72,14 +75,12 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
         wave_sync();
         u4v q[8];
         stage_chunks(stage, wv, lane, q);
-        const int nb = nblk - (int)(b * 64) < 64 ? nblk - (int)(b * 64) : 64;
+        const int nb = (int)out.nb;
         {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128, (short)0, nb * 128, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, nb * 128, 0x00020000);
 #pragma unroll
             for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(q[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
         }
-        uint32_t *off = offsets + es.blk_first[k] + (size_t)b * 64;
         uint32_t run = 0;
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {

@@ -289,7 +289,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     // global batch g -> plane k, plane-local batch b (wave-uniform)
     const int k = plane_of(ps, g);
     const PlaneArgs &p = ps.pl[k];
-    const uint32_t b = g - ps.first[k];
+    const uint32_t b = g - first_of(ps, k);
     int16_t *__restrict__ coef = ps.coef[k];
     int32_t *__restrict__ var_out = ps.var[k];
     uint2 cur[8];
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v2(PlaneSet ps, Fast
     uint2 nxt[8];
     {
         const int k0 = plane_of(ps, g);
-        load_rows(ps.pl[k0], (g - ps.first[k0]) * 64 + lane, nxt);
+        load_rows(ps.pl[k0], (g - first_of(ps, k0)) * 64 + lane, nxt);
     }
     // same fence as at the end of a batch: the loop header then sees no load in
     // flight on either incoming edge and needs no wait at all
@@ -558,11 +558,12 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         const uint32_t gnext = g + step;
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];
-        const uint32_t b = g - ps.first[k];
+        const uint32_t b = g - first_of(ps, k);
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         prefetch_batch(ps, gnext, lane, nxt);
+        const BatchOut out = batch_out(ps, k, b);
         int32_t var_num;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)p.nblk, var_num, mlo,
@@ -578,15 +579,13 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         wave_sync();
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
-        const uint32_t left = (uint32_t)p.nblk - b * 64;
-        const uint32_t nb = left < 64u ? left : 64u;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(out.nb * 128u), 0x00020000);
 #pragma unroll
         for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_STORE_AUX);
         if (VAR) {
             const __amdgpu_buffer_rsrc_t rv =
-                __builtin_amdgcn_make_buffer_rsrc(ps.var[k] + (size_t)b * 64, (short)0, (int)(nb * 4u), 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(out.nb * 4u), 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_STORE_AUX);
         }
     }
@@ -672,12 +671,12 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, cons
     }
     for (; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
-        const PlaneArgs &p = ps.pl[k];
-        const uint32_t b = g - ps.first[k];
+        const uint32_t b = g - first_of(ps, k);
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         prefetch_batch(ps, g + step, lane, nxt);
+        const BatchOut out = batch_out(ps, k, b);
         // fdct8_compute's stage writes: dword i*4 + cp of the lane's 136-B slot
         uint32_t *st32 = reinterpret_cast<uint32_t *>(stage) + (wv * 64 + lane) * (kPitch2 / 4);
         if (DCTQ_MV3_B64) {  // A/B: 16 b64 writes (fdct8_movement_v2's)
@@ -699,10 +698,8 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, cons
         wave_sync();
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
-        const uint32_t left = (uint32_t)p.nblk - b * 64;
-        const uint32_t nb = left < 64u ? left : 64u;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<char *>(coef_of(ps, k)) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(out.nb * 128u), 0x00020000);
 #pragma unroll
         for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_STORE_AUX);
     }
@@ -720,14 +717,14 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement_v2(PlaneSet ps) {
     uint2 nxt[8];
     {
         const int k0 = plane_of(ps, g);
-        load_rows(ps.pl[k0], (g - ps.first[k0]) * 64 + lane, nxt);
+        load_rows(ps.pl[k0], (g - first_of(ps, k0)) * 64 + lane, nxt);
     }
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
     for (; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];
-        const uint32_t b = g - ps.first[k];
+        const uint32_t b = g - first_of(ps, k);
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];

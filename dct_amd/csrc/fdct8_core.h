@@ -145,6 +145,16 @@ __device__ __forceinline__ int16_t *coef_of(const PlaneSet &ps, uint32_t k) {
     return c;
 }
 
+// First global batch of plane k (wave-uniform k): a select chain over the batch
+// prefixes, which sit in SGPRs for the whole kernel -- an indexed kernel-argument
+// load here was one more scalar-cache round trip in front of every prefetch.
+__device__ __forceinline__ uint32_t first_of(const PlaneSet &ps, int k) {
+    uint32_t f = 0u;
+#pragma unroll
+    for (int i = 1; i < kMaxPlanes; ++i) f = k == i ? ps.first[i] : f;
+    return f;
+}
+
 // Plane of global batch g (wave-uniform).
 __device__ __forceinline__ int plane_of(const PlaneSet &ps, uint32_t g) {
     int k = 0;
@@ -627,6 +637,29 @@ __device__ __forceinline__ void stage_chunks(const uint4 *stage, int wv, int lan
     }
 }
 
+// A batch's coefficient destination (plane k's output + its 64-block batch b, and the
+// blocks it holds), resolved where it is called.  DCTQ_PIN_OUT pins the values in
+// SGPRs there: without it LLVM re-issues their kernel-argument loads after the
+// prefetch fence (an asm with a "memory" clobber), so a scalar-cache round trip sits
+// between the rows' arrival and the stores of every batch.
+#ifndef DCTQ_PIN_OUT
+#define DCTQ_PIN_OUT 1
+#endif
+struct BatchOut {
+    char *base;   // output of block 0 of the batch
+    int32_t *var; // var_num of block 0 of the batch (if the plane set has var_num outputs)
+    uint32_t nb;  // valid blocks in the batch
+};
+__device__ __forceinline__ BatchOut batch_out(const PlaneSet &ps, int k, uint32_t b) {
+    const uint32_t left = (uint32_t)ps.pl[k].nblk - b * 64;
+    BatchOut o;
+    o.nb = left < 64u ? left : 64u;
+    o.base = reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128;
+    o.var = ps.var[k] ? ps.var[k] + (size_t)b * 64 : nullptr;
+    if (DCTQ_PIN_OUT) asm volatile("" : "+s"(o.nb), "+s"(o.base), "+s"(o.var));
+    return o;
+}
+
 // vmcnt(0): the wave's stores have read their data VGPRs (and left the CU).
 __device__ __forceinline__ void retire_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
@@ -642,7 +675,7 @@ template <bool SKIP = true>
 __device__ __forceinline__ void prefetch_batch(const PlaneSet &ps, uint32_t gn, int lane, uint2 (&nxt)[8]) {
     if (SKIP && DCTQ_SKIP_TAIL_PF && gn >= ps.first[ps.n]) return;  // wave-uniform
     const int kn = plane_of(ps, gn);
-    load_rows(ps.pl[kn], (gn - ps.first[kn]) * 64 + lane, nxt);
+    load_rows(ps.pl[kn], (gn - first_of(ps, kn)) * 64 + lane, nxt);
 }
 
 }  // namespace dctq

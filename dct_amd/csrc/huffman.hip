@@ -888,7 +888,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
     for (uint32_t g = blockIdx.x * kHufWaves + wv; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];
-        const uint32_t b = g - ps.first[k];
+        const uint32_t b = g - first_of(ps, k);
         const uint32_t n = b * 64 + lane;
         const bool valid = n < (uint32_t)p.nblk;
         const int nb = (uint32_t)p.nblk - b * 64 < 64u ? (int)((uint32_t)p.nblk - b * 64) : 64;
@@ -916,6 +916,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
             wave_sync();
         }
         const uint32_t out = tile_bits<true>(mine, ctr, lane, wv, nb, [] {});
+        // (pinning this destination in SGPRs at the top, as the forward kernels do, spilled 8 B here)
         const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
             bits + es.blk_first[k] + (size_t)b * 64, (short)0, nb * 4, 0x00020000);
         __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);

@@ -122,12 +122,15 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
     for (; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];
-        const uint32_t b = g - ps.first[k];
+        const uint32_t b = g - first_of(ps, k);
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
         if (DCTQ_RT_EARLY_PREFETCH) prefetch_batch<false>(ps, g + step, lane, nxt);
+        const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
+        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
+        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
 
         // ---- 1. forward into the stage; ties resolved in place
         int32_t var_num;
@@ -140,8 +143,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         wave_sync();
 
         // ---- 2. read-back: coefficient chunks + the inverse's half blocks
-        const uint32_t left = (uint32_t)p.nblk - b * 64;
-        const uint32_t nb = left < 64u ? left : 64u;
+        const uint32_t nb = out.nb;
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
         const uint2 *st64 = reinterpret_cast<const uint2 *>(wstage);
@@ -159,20 +161,18 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         // lanes j / 32+j: var of block j in x, of block 32+j in y
         const auto vv = __builtin_amdgcn_permlane32_swap((uint32_t)var_num, (uint32_t)var_num, false, false);
         {
-            int16_t *coef = ps.coef[k];
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<char *>(coef) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
 #pragma unroll
             for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
             if (VAR) {
                 const __amdgpu_buffer_rsrc_t rv =
-                    __builtin_amdgcn_make_buffer_rsrc(ps.var[k] + (size_t)b * 64, (short)0, (int)(nb * 4u), 0x00020000);
+                    __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(nb * 4u), 0x00020000);
                 __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_NT_AUX);
             }
         }
 
         // ---- 3. paired fp64 inverses, blocks 0-31 then 32-63 of the batch
-        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         char *mine = wstage + j * kPitchP + h * 128;
         inverse_half<ADAPTIVE>(dev, qa, (int32_t)vv[0], h, mine);
         retire_stores();
@@ -234,12 +234,14 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(Roun
     char *wstage = reinterpret_cast<char *>(stage) + wv * 64 * kPitch2;
     for (; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
-        const PlaneArgs &p = ps.pl[k];
-        const uint32_t b = g - ps.first[k];
+        const uint32_t b = g - first_of(ps, k);
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         prefetch_batch<false>(ps, g + step, lane, nxt);
+        const BatchOut out = batch_out(ps, k, b);
+        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
+        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
         uint2 *mine2 = reinterpret_cast<uint2 *>(wstage + lane * kPitch2);
         retire_stores();
 #pragma unroll
@@ -248,17 +250,15 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(Roun
             mine2[2 * r + 1] = make_uint2(cur[r].y, cur[r].x);
         }
         wave_sync();
-        const uint32_t left = (uint32_t)p.nblk - b * 64;
-        const uint32_t nb = left < 64u ? left : 64u;
+        const uint32_t nb = out.nb;
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
         {
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
 #pragma unroll
             for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
         }
-        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         char *mine = wstage + j * kPitchP + h * 128;
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
