@@ -290,14 +290,13 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     const int k = plane_of(ps, g);
     const PlaneArgs &p = ps.pl[k];
     const uint32_t b = g - first_of(ps, k);
-    int16_t *__restrict__ coef = ps.coef[k];
-    int32_t *__restrict__ var_out = ps.var[k];
     uint2 cur[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
     const uint32_t n = b * 64 + lane;
     const bool valid = n < (uint32_t)p.nblk;
     prefetch_batch(ps, g + step, lane, nxt);
+    const BatchOut out = batch_out(ps, k, b);
 
     uint32_t mlo, mhi;
     int32_t var_num;
@@ -345,10 +344,8 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
         // valid block: out-of-range lanes are dropped by the hardware, so the
         // stores are unconditional (predicated stores made the waitcnt pass give
         // up and wait vmcnt(0) at the loop latch).
-        const uint32_t left = (uint32_t)p.nblk - b * 64;
-        const uint32_t nb = left < 64u ? left : 64u;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            reinterpret_cast<char *>(coef) + (size_t)b * 64 * 128, (short)0, (int)(nb * 128u), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(out.nb * 128u), 0x00020000);
         const uint2 *st64 = reinterpret_cast<const uint2 *>(stage) + wv * 64 * (kPitch2 / 8);
         // all 8 chunks into distinct registers first, one voffset register and
         // per-store soffsets: a store's VGPR operands must not be overwritten
@@ -370,7 +367,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
         }
         if (VAR) {
             const __amdgpu_buffer_rsrc_t rv =
-                __builtin_amdgcn_make_buffer_rsrc(var_out + (size_t)b * 64, (short)0, (int)(nb * 4u), 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(out.nb * 4u), 0x00020000);
             __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_STORE_AUX);
         }
     }
