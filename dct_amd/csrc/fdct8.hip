@@ -272,6 +272,12 @@ __device__ __forceinline__ void drain_queue(const PlaneSet &ps, const DevTables 
 #ifndef DCTQ_LAST_INPLACE
 #define DCTQ_LAST_INPLACE 1  // a wave's last batch empties the queue before its stores and resolves in place
 #endif
+#ifndef DCTQ_V2_GROUP
+#define DCTQ_V2_GROUP 0  // A/B: the in-stage passes of the queue kernel in grouped rounds (resolve_ties_compact GROUP8)
+#endif
+#ifndef DCTQ_V2_WIDE
+#define DCTQ_V2_WIDE 3   // ... and with the 4- / 2-lane rounds when DCTQ_V2_GROUP
+#endif
 #ifndef DCTQ_INSTAGE_LANES
 // A batch with at least this many flagged blocks resolves its ties in the stage,
 // before its stores (resolve_in_stage); sparser batches queue them.  65 = never.
@@ -332,7 +338,7 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
     if ((DCTQ_INSTAGE_LANES <= 64 && nflag >= DCTQ_INSTAGE_LANES) || (last && nflag > 0))
     {
         // tie-heavy batch: resolved in the stage before its stores (no stash, no patches)
-        const uint32_t n = resolve_ties_compact<ADAPTIVE>(tab, cur, stage, qc + qn, lane, wv, mlo, mhi);
+        const uint32_t n = resolve_ties_compact<ADAPTIVE, DCTQ_V2_GROUP, DCTQ_V2_GROUP ? DCTQ_V2_WIDE : 0>(tab, cur, stage, qc + qn, lane, wv, mlo, mhi);
         if (STATS && n) atomicAdd(fallbacks, (unsigned long long)n);
     }
 
