@@ -104,6 +104,8 @@ for step in "$@"; do
     abfo) run abfo 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_prev.so tools/ubench/libvar_pin0.so tools/ubench/libvar_g32.so movement movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_prev.so tools/ubench/libvar_pin0.so tools/ubench/libvar_g32.so movement movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_prev.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_prev.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 default tools/ubench/libvar_prev.so tools/ubench/libvar_g32.so movement8" ;;
     abgrid) run abgrid 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind const default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so && python tools/lib_ab.py --rounds 8 --b2b 3 --frames 4 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so" ;;
     abv2g) run abv2g 900 bash -c "python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 --kind smooth default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 99 --adaptive 1 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 99 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 97 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 --kind extreme default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8" ;;
+    collect) run collect 1100 bash tools/collect_profiles.sh ;;
+    probe) run probe 400 bash -c "python tools/lib_order_probe.py product && python tools/lib_order_probe.py diag && python tools/lib_order_probe.py both && python tools/lib_order_probe.py streams && python tools/lib_order_probe.py both 50 && python tools/lib_order_probe.py diag && python tools/lib_order_probe.py product" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
