@@ -581,15 +581,26 @@ LEG_PREWARM_MS = 30.0
 def timed_steady(fn, steps, dev, prewarm_ms=LEG_PREWARM_MS):
     """Wall time of `steps` back-to-back calls of a secondary leg's step, measured
     the way the headline is (main()): the step first runs back to back, untimed,
-    for `prewarm_ms` -- between legs the GPU idles while the host works, and an
-    idle MI355X drops its clocks within milliseconds -- then the
+    for about `prewarm_ms` -- between legs the GPU idles while the host works, and
+    an idle MI355X drops its clocks within milliseconds -- then the
     timed steps are bracketed by a barrier and a synchronize on both sides; the
-    max over ranks."""
-    t_pre = time.perf_counter()
-    while (time.perf_counter() - t_pre) * 1e3 < prewarm_ms:
-        for _ in range(4):
-            fn()
-        torch.cuda.synchronize()
+    max over ranks.  The pre-warm is a COUNT of calls that every rank agrees on
+    (one timed call, the max over ranks of the count it suggests): a step may hold
+    collectives (the symbol-stream gather), so every rank must call it equally often."""
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    one = max(time.perf_counter() - t, 1e-6)
+    n_pre = min(400, max(1, int(prewarm_ms * 1e-3 / one)))
+    if dist.is_initialized():
+        n = torch.tensor([n_pre], dtype=torch.int64, device=dev)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX)
+        n_pre = int(n.item())
+    for i in range(n_pre):
+        fn()
+        if i % 4 == 3:
+            torch.cuda.synchronize()
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()

@@ -106,6 +106,8 @@ for step in "$@"; do
     abv2g) run abv2g 900 bash -c "python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 --kind smooth default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 99 --adaptive 1 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 99 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 97 default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 --kind extreme default tools/ubench/libvar_ctl.so tools/ubench/libvar_v2gw.so movement8" ;;
     collect) run collect 1100 bash tools/collect_profiles.sh ;;
     probe) run probe 400 bash -c "python tools/lib_order_probe.py product && python tools/lib_order_probe.py diag && python tools/lib_order_probe.py both && python tools/lib_order_probe.py streams && python tools/lib_order_probe.py both 50 && python tools/lib_order_probe.py diag && python tools/lib_order_probe.py product" ;;
+    testdist) run pytest_dist 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "gpus2 or dist_legs or bench_json" ;;
+    matrix2) run matrix2 400 python tools/perf_matrix.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,6 +1,9 @@
 """Forward DCT+quant over the bench's step (64 4K luma + 128 1080p chroma planes, one
 multi-plane launch) for every input kind x plan, each next to the no-arithmetic
-movement of the same planes (dctq_diag_movement_planes) on the same box:
+movement of the same planes (dctq_diag_movement_planes) on the same box.  The
+forward runs through the product library (libdct_amd.so), the movement through
+the diagnostic one (round 4: through the diagnostic library the tie-heavy rows
+read 5-8 % slower):
 HIP events, medians of samples of 3 launches back to back after one untimed
 launch of the same kind (steady state: profiles/r02/policy_b2b.md).  Prints one
 line per configuration.
@@ -44,7 +47,7 @@ def timed(fn, reps=8, b2b=3):
 # which the first configuration's samples would otherwise absorb
 _y = dct_amd.synth(1, "uniform", 3840, 2160, F)
 _c = dct_amd.synth(2, "uniform", 1920, 1080, 2 * F)
-_p = dct_amd.Plan(50, 0, diagnostic=True)
+_p = dct_amd.Plan(50, 0)
 _t = time.perf_counter()
 while time.perf_counter() - _t < 0.3:
     for _ in range(8):
@@ -58,7 +61,8 @@ for kind in ("uniform", "smooth", "const", "extreme"):
     y = dct_amd.synth(12345, kind, 3840, 2160, F)
     c = dct_amd.synth(62345, kind, 1920, 1080, 2 * F)
     for q, ad in ((50, 0), (90, 0), (50, 1), (10, 0), (100, 0)):
-        plan = dct_amd.Plan(q, ad, diagnostic=True)
+        plan = dct_amd.Plan(q, ad)
+        dplan = dct_amd.Plan(q, ad, diagnostic=True)
         fb.zero_()
         plan.set_fallback_counter(fb)
         plan.forward_quant_planes([y, c], outs=[oy, oc])
@@ -66,7 +70,7 @@ for kind in ("uniform", "smooth", "const", "extreme"):
         ties = int(fb.item()) / n
         plan.set_fallback_counter(None)
         tf = timed(lambda: plan.forward_quant_planes([y, c], outs=[oy, oc]))
-        tm = timed(lambda: plan.diag_movement_planes([y, c], [oy, oc]))
+        tm = timed(lambda: dplan.diag_movement_planes([y, c], [oy, oc]))
         gf, gm = n * 192 / tf / 8e12 * 100, n * 192 / tm / 8e12 * 100
         print(f"{kind:8s} q{q}a{ad:<5d} {tf * 1e6:10.1f} {gf:8.1f} {tm * 1e6:10.1f} {gm:8.1f} {tm / tf:8.3f} "
               f"{ties:8.4f}", flush=True)
