@@ -108,6 +108,9 @@ for step in "$@"; do
     probe) run probe 400 bash -c "python tools/lib_order_probe.py product && python tools/lib_order_probe.py diag && python tools/lib_order_probe.py both && python tools/lib_order_probe.py streams && python tools/lib_order_probe.py both 50 && python tools/lib_order_probe.py diag && python tools/lib_order_probe.py product" ;;
     testdist) run pytest_dist 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "gpus2 or dist_legs or bench_json" ;;
     matrix2) run matrix2 400 python tools/perf_matrix.py ;;
+    aux2) run aux2 300 python tools/aux_bench.py ;;
+    profaux2) run profaux2 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profaux2 -o run --output-format csv -- python tools/aux_bench.py ;;
+    huf2) run huf2 300 python tools/huf_ab.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
