@@ -9,6 +9,7 @@ import ctypes as C
 import glob
 import os
 import statistics
+import time
 import sys
 
 import torch
@@ -30,15 +31,24 @@ for kind in ("uniform", "smooth", "const", "extreme"):
     out = torch.zeros(nblk, dtype=torch.int32, device="cuda")  # shared by every build (see tools/rle_ab.py)
     ref = None
     times = {k: [] for k in libs}
+    t_pre = time.perf_counter()  # ~30 ms of launches back to back first: an idle box drops its clocks
+    while time.perf_counter() - t_pre < 0.03:
+        for _ in range(4):
+            assert libs["default"].dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(out.data_ptr()), s) == 0
+        torch.cuda.synchronize()
     for r in range(9):
         for k, L in libs.items():
+            # steady state: one untimed launch, then 3 back to back (the bench's method)
+            launch = lambda: L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(out.data_ptr()), s)
+            assert launch() == 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            assert L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(out.data_ptr()), s) == 0
+            for _ in range(3):
+                assert launch() == 0
             e1.record()
             torch.cuda.synchronize()
             if r:
-                times[k].append(e0.elapsed_time(e1) * 1e-3)
+                times[k].append(e0.elapsed_time(e1) * 1e-3 / 3)
             elif ref is None:
                 ref = out.clone()
             elif not k.startswith("no"):  # libvar_no*.so: timing ablations, outputs knowingly wrong
