@@ -111,6 +111,7 @@ for step in "$@"; do
     aux2) run aux2 300 python tools/aux_bench.py ;;
     profaux2) run profaux2 400 rocprofv3 --kernel-trace --stats -d gpurun_out/profaux2 -o run --output-format csv -- python tools/aux_bench.py ;;
     huf2) run huf2 300 python tools/huf_ab.py ;;
+    rehearse8) run rehearse8 600 python bench.py --gpus 8 --backend gloo --frames 4 --total-frames 8 --no-cpu --ceiling-rounds 2 --steps 5 --warmup 2 --encode-steps 3 --round-trip-steps 3 --gather-steps 2 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
