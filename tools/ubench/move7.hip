@@ -6,6 +6,8 @@
 //         r of block b at r * 512 + 8 b: b128 writes and b64 reads conflict-free)
 //         into the lane-per-block registers, then the same 136-B stage and stores.
 //         Pairs of blocks never straddle a block row here (480 / 240 blocks per row).
+// rows8 direct: no stage, each lane stores its block (8 x 16 B at a 128-B lane stride).
+// flat staged: the flat stream's loads with the product's stage and stores.
 // Same bytes, method and items as move6 (steady state, interleaved, HIP events).
 // Build: hipcc --offload-arch=gfx950 -O3 -Iinclude -Ldct_amd -ldct_amd_diag
 //        -Wl,-rpath,'$ORIGIN/../../dct_amd' -o tools/ubench/move7 tools/ubench/move7.hip
@@ -185,6 +187,80 @@ __global__ __launch_bounds__(256) void k_pair16(Geo g) {
     }
 }
 
+// rows8 loads, no stage: lane b stores its own block's 128 B as 8 x 16 B (instruction k
+// writes bytes 16k.. of every block: 64 x 16 B at a 128-B stride)
+__global__ __launch_bounds__(256) void k_rows8_direct(Geo g) {
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t step = gridDim.x * 4;
+    uint32_t it = blockIdx.x * 4 + wv;
+    uint2 nxt[8];
+    if (it < g.nbatch) load_rows(g, it, lane, nxt);
+    pin(nxt);
+    for (; it < g.nbatch; it += step) {
+        uint2 cur[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+        if (it + step < g.nbatch) load_rows(g, it + step, lane, nxt);
+        pin(nxt);
+        const int pl = it >= g.p[0].nbatch;
+        const Plane &P = pl ? g.p[1] : g.p[0];
+        const uint32_t lb = it - (pl ? g.p[0].nbatch : 0);
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(P.dst + (size_t)lb * 8192, 0, 8192, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            __builtin_amdgcn_raw_buffer_store_b128(u4v{cur[k].x, cur[k].y, cur[k].y, cur[k].x}, rc, lane * 128, k * 16, 2);
+    }
+}
+
+// flat loads (4 x 16 B per lane = the batch's 4 KiB of pixels in order), the product's
+// 136-B stage writes and 8 x 1 KiB stores: rows8 with the load shape of the flat stream
+__global__ __launch_bounds__(256) void k_flat_staged(const u4v *src, Geo g) {
+    __shared__ uint4 st[256 * 136 / 16 + 96];
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t step = gridDim.x * 4;
+    uint32_t it = blockIdx.x * 4 + wv;
+    u4v nxt[4];
+    if (it < g.nbatch)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nxt[j] = __builtin_nontemporal_load(src + (size_t)it * 256 + j * 64 + lane);
+    pin4(nxt);
+    char *ws = reinterpret_cast<char *>(st) + wv * 8704;
+    for (; it < g.nbatch; it += step) {
+        uint2 cur[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            cur[2 * j] = make_uint2(nxt[j].x, nxt[j].y);
+            cur[2 * j + 1] = make_uint2(nxt[j].z, nxt[j].w);
+        }
+        if (it + step < g.nbatch)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) nxt[j] = __builtin_nontemporal_load(src + (size_t)(it + step) * 256 + j * 64 + lane);
+        uint2 *mine = reinterpret_cast<uint2 *>(ws + lane * 136);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            mine[2 * k] = cur[k];
+            mine[2 * k + 1] = make_uint2(cur[k].y, cur[k].x);
+        }
+        pin4(nxt);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        u4v val[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int m = k * 64 + lane, bl = m >> 3;
+            const uint2 *s2 = reinterpret_cast<const uint2 *>(ws + bl * 136 + (m & 7) * 16);
+            val[k] = u4v{s2[0].x, s2[0].y, s2[1].x, s2[1].y};
+        }
+        const int pl = it >= g.p[0].nbatch;
+        const Plane &P = pl ? g.p[1] : g.p[0];
+        const uint32_t lb = it - (pl ? g.p[0].nbatch : 0);
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(P.dst + (size_t)lb * 8192, 0, 8192, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rc, lane * 16, k * 1024, 2);
+    }
+}
+
 __global__ void k_fill(uint32_t *p, size_t n, uint32_t seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull + seed;
@@ -237,6 +313,12 @@ int main(int argc, char **argv) {
                          [=] { hipLaunchKernelGGL(k_rows8, dim3(cus * 4 * m), dim3(256), 0, 0, g2); }});
         items.push_back({"pair16 2out x" + std::to_string(m),
                          [=] { hipLaunchKernelGGL(k_pair16<0>, dim3(cus * 4 * m), dim3(256), 0, 0, g2); }});
+    }
+    for (int m : {16, 32}) {
+        items.push_back({"rows8 direct x" + std::to_string(m),
+                         [=] { hipLaunchKernelGGL(k_rows8_direct, dim3(cus * 4 * m), dim3(256), 0, 0, g2); }});
+        items.push_back({"flat staged x" + std::to_string(m),
+                         [=] { hipLaunchKernelGGL(k_flat_staged, dim3(cus * 4 * m), dim3(256), 0, 0, (const u4v *)src, g2); }});
     }
     items.push_back({"fwd 2out", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, c2, nullptr, nullptr)); }});
     items.push_back({"mv 2out x16", [=] { DCHECK(dctq_diag_movement_grid_planes(plan, planes, 2, c2, 16, nullptr)); }});
