@@ -101,6 +101,7 @@ for step in "$@"; do
     abwt) run abwt 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so movement movement8 movement:tools/ubench/libvar_mwt.so movement:tools/ubench/libvar_mwt32.so && python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so movement movement8 movement:tools/ubench/libvar_mwt.so movement:tools/ubench/libvar_mwt32.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_wt.so tools/ubench/libvar_wt24.so tools/ubench/libvar_wt32.so tools/ubench/libvar_g24.so" ;;
     move6) run move6 300 tools/ubench/move6 12 3 ;;
     move7) run move7 300 tools/ubench/move7 12 3 ;;
+    move8) run move8 300 tools/ubench/move8 12 3 ;;
     abpin) run abpin 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_pin.so movement movement:tools/ubench/libvar_mpin.so movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_pin.so movement movement:tools/ubench/libvar_mpin.so movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_pin.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_pin.so" ;;
     abfo) run abfo 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_prev.so tools/ubench/libvar_pin0.so tools/ubench/libvar_g32.so movement movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_prev.so tools/ubench/libvar_pin0.so tools/ubench/libvar_g32.so movement movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_prev.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_prev.so tools/ubench/libvar_g32.so && python tools/lib_ab.py --rounds 8 --b2b 3 --quality 100 default tools/ubench/libvar_prev.so tools/ubench/libvar_g32.so movement8" ;;
     abgrid) run abgrid 900 bash -c "python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement movement8 && python tools/lib_ab.py --rounds 10 --b2b 3 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so movement movement8 && python tools/lib_ab.py --rounds 8 --b2b 3 --kind extreme --quality 10 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind smooth --quality 90 --adaptive 1 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so && python tools/lib_ab.py --rounds 8 --b2b 3 --kind const default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so && python tools/lib_ab.py --rounds 8 --b2b 3 --frames 4 default tools/ubench/libvar_g24.so tools/ubench/libvar_g32.so tools/ubench/libvar_g48.so" ;;
