@@ -6,7 +6,8 @@
 //   LOAD  0 rows8 (8 x 8 B per lane: block rows) / 1 flat16 (4 x 16 B per lane)
 //   STAGE 0 stores from registers (flat16 only) / 1 the product's 136-B stage
 //   PF    0 load at the loop top / 1 next batch prefetched before the stores
-// on grids of CUs x 4 x {16, 32, 48} workgroups of 4 waves; steady state,
+// on grids of CUs x 4 x {16, 32, 48} workgroups of 4 waves, writing the outputs of two
+// allocations (g2, as bench.py) or one (out1 right after the pixels, outZ allocated last); steady state,
 // interleaved rounds, HIP events, medians (as move6/move7).
 // Build: hipcc --offload-arch=gfx950 -O3 -Iinclude -Ldct_amd -ldct_amd_diag
 //        -Wl,-rpath,'$ORIGIN/../../dct_amd' -o tools/ubench/move8 tools/ubench/move8.hip
@@ -174,17 +175,25 @@ int main(int argc, char **argv) {
     int cus = 0;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     uint8_t *src;
-    char *out1, *outY, *outC;
+    char *out1, *outY, *outC, *outZ;
     CHECK(hipMalloc(&src, ybytes + cbytes));
     CHECK(hipMalloc(&out1, nblk * 128));
     CHECK(hipMalloc(&outY, nby * 128));
     CHECK(hipMalloc(&outC, nbc * 128));
+    CHECK(hipMalloc(&outZ, nblk * 128));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (uint32_t *)src, (ybytes + cbytes) / 4, 12345u);
     CHECK(hipDeviceSynchronize());
     Geo g2;
     g2.p[0] = Plane{src, outY, 480, 129600, 3840, (uint32_t)(ybytes / 4096), (size_t)3840 * 2160};
     g2.p[1] = Plane{src + ybytes, outC, 240, 32400, 1920, (uint32_t)(cbytes / 4096), (size_t)1920 * 1080};
     g2.nbatch = g2.p[0].nbatch + g2.p[1].nbatch;
+    // g1: both planes' outputs in out1 (allocated right after the pixels, as dctq_diag_stream's
+    // dst in this program); gz: in outZ (allocated last)
+    Geo g1 = g2, gz = g2;
+    g1.p[0].dst = out1;
+    g1.p[1].dst = out1 + nby * 128;
+    gz.p[0].dst = outZ;
+    gz.p[1].dst = outZ + nby * 128;
     const u4v *flat = (const u4v *)src;
     dctq_plan *plan = nullptr;
     DCHECK(dctq_plan_create(50, 0, &plan));
@@ -210,6 +219,19 @@ int main(int argc, char **argv) {
         items.push_back({"flat16 regs pf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 1>), gr, dim3(256), 0, 0, g2, flat); }});
         items.push_back({"flat16 regs nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 0>), gr, dim3(256), 0, 0, g2, flat); }});
     }
+    for (int o = 1; o <= 2; ++o) {
+        const Geo gg = o == 1 ? g1 : gz;
+        const std::string t = o == 1 ? " out1" : " outZ";
+        const dim3 g16(cus * 4 * 16), g32(cus * 4 * 32);
+        items.push_back({"rows8  stage pf x16" + t, [=] { hipLaunchKernelGGL((k_move<0, 1, 1>), g16, dim3(256), 0, 0, gg, flat); }});
+        items.push_back({"flat16 stage nopf x32" + t, [=] { hipLaunchKernelGGL((k_move<1, 1, 0>), g32, dim3(256), 0, 0, gg, flat); }});
+        items.push_back({"flat16 regs nopf x32" + t, [=] { hipLaunchKernelGGL((k_move<1, 0, 0>), g32, dim3(256), 0, 0, gg, flat); }});
+    }
+    int16_t *c1[2] = {(int16_t *)out1, (int16_t *)(out1 + nby * 128)};
+    int16_t *cz[2] = {(int16_t *)outZ, (int16_t *)(outZ + nby * 128)};
+    items.push_back({"fwd q50 out1", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, c1, nullptr, nullptr)); }});
+    items.push_back({"fwd q50 outZ", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, cz, nullptr, nullptr)); }});
+    items.push_back({"diag flat kind 7 -> outZ", [=] { DCHECK(dctq_diag_stream(7, src, outZ, (long long)nblk / 64 * 64, nullptr)); }});
     items.push_back({"fwd q50", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, c2, nullptr, nullptr)); }});
     items.push_back({"diag flat kind 7 (1 out)", [=] { DCHECK(dctq_diag_stream(7, src, out1, (long long)nblk / 64 * 64, nullptr)); }});
     for (int w = 0; w < 300; ++w) items[w % items.size()].fn();  // clock pre-warm
