@@ -3,7 +3,9 @@
 // 1:2 stream that beats it by 2-4 % on median boxes (dctq_diag_stream kind 7: 16-B
 // loads, stores straight from the loaded registers, no prefetch, one batch per wave).
 // One kernel template over the three differences, same bytes and buffers:
-//   LOAD  0 rows8 (8 x 8 B per lane: block rows) / 1 flat16 (4 x 16 B per lane)
+//   LOAD  0 rows8 (8 x 8 B per lane: block rows) / 1 flat16 (4 x 16 B per lane: NOT the
+//         batch's blocks, the bytes in memory order) / 2 pair16 (16 B per lane: row 2j + h of
+//         blocks 2p, 2p + 1, transposed through the stage into lane-per-block rows, move7)
 //   STAGE 0 stores from registers (flat16 only) / 1 the product's 136-B stage
 //   PF    0 load at the loop top / 1 next batch prefetched before the stores
 // on grids of CUs x 4 x {16, 32, 48} workgroups of 4 waves, writing the outputs of two
@@ -93,9 +95,16 @@ __device__ __forceinline__ void load_batch(const Geo &g, const u4v *flat, uint32
         load_rows(g, b, lane, rows);
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = u4v{rows[2 * j].x, rows[2 * j].y, rows[2 * j + 1].x, rows[2 * j + 1].y};
-    } else {
+    } else if constexpr (LOAD == 1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = __builtin_nontemporal_load(flat + (size_t)b * 256 + j * 64 + lane);
+    } else {  // pair16: lane (p, h) loads row 2j + h of blocks 2p, 2p + 1
+        const int pl = b >= g.p[0].nbatch;
+        const Plane &P = pl ? g.p[1] : g.p[0];
+        const int p = lane & 31, h = lane >> 5;
+        const uint8_t *px = blk(P, (b - (pl ? g.p[0].nbatch : 0)) * 64 + 2 * p) + h * P.stride;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = __builtin_nontemporal_load((const u4v *)(px + 2 * j * P.stride));
     }
 }
 
@@ -121,6 +130,18 @@ __global__ __launch_bounds__(256) void k_move(Geo g, const u4v *flat) {
             if (it + step < g.nbatch) load_batch<LOAD>(g, flat, it + step, lane, nxt);
         } else {
             load_batch<LOAD>(g, flat, it, lane, cur);
+        }
+        if constexpr (LOAD == 2) {  // rows -> LDS (row r at r * 512), then lane-per-block rows
+            const int p = lane & 31, h = lane >> 5;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) *reinterpret_cast<u4v *>(ws + (2 * j + h) * 512 + p * 16) = cur[j];
+            wsync();
+            uint2 rw[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) rw[k] = *reinterpret_cast<const uint2 *>(ws + k * 512 + lane * 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cur[j] = u4v{rw[2 * j].x, rw[2 * j].y, rw[2 * j + 1].x, rw[2 * j + 1].y};
+            wsync();
         }
         const int pl = it >= g.p[0].nbatch;
         const Plane &P = pl ? g.p[1] : g.p[0];
@@ -218,6 +239,12 @@ int main(int argc, char **argv) {
         items.push_back({"flat16 stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
         items.push_back({"flat16 regs pf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 1>), gr, dim3(256), 0, 0, g2, flat); }});
         items.push_back({"flat16 regs nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 0>), gr, dim3(256), 0, 0, g2, flat); }});
+    }
+    for (int m : {16, 32}) {
+        const dim3 gr(cus * 4 * m);
+        const std::string x = " x" + std::to_string(m);
+        items.push_back({"pair16 stage pf" + x, [=] { hipLaunchKernelGGL((k_move<2, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"pair16 stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<2, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
     }
     for (int o = 1; o <= 2; ++o) {
         const Geo gg = o == 1 ? g1 : gz;
