@@ -10,7 +10,8 @@
 //   PF    0 load at the loop top / 1 next batch prefetched before the stores
 // on grids of CUs x 4 x {16, 32, 48} workgroups of 4 waves, writing the outputs of two
 // allocations (g2, as bench.py) or one (out1 right after the pixels, outZ allocated last); steady state,
-// interleaved rounds, HIP events, medians (as move6/move7).
+// interleaved rounds, HIP events, medians (as move6/move7).  ORD: the order of the 8 x 1 KiB
+// stores (chunks 0..7, or 0, 4, 1, 5, .. as dctq_diag_stream).  profiles/r04/move8_*.log.
 // Build: hipcc --offload-arch=gfx950 -O3 -Iinclude -Ldct_amd -ldct_amd_diag
 //        -Wl,-rpath,'$ORIGIN/../../dct_amd' -o tools/ubench/move8 tools/ubench/move8.hip
 #include <hip/hip_runtime.h>
@@ -112,7 +113,7 @@ __device__ __forceinline__ void pin4(u4v (&r)[4]) {
     asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3])::"memory");
 }
 
-template <int LOAD, int STAGE, int PF>
+template <int LOAD, int STAGE, int PF, int ORD = 0>
 __global__ __launch_bounds__(256) void k_move(Geo g, const u4v *flat) {
     __shared__ uint4 st[256 * 136 / 16 + 96];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -173,7 +174,10 @@ __global__ __launch_bounds__(256) void k_move(Geo g, const u4v *flat) {
             }
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rc, lane * 16, k * 1024, 2);
+        for (int i = 0; i < 8; ++i) {  // ORD 0: chunks 0..7; ORD 1: 0, 4, 1, 5, 2, 6, 3, 7 (dctq_diag_stream's order)
+            const int k = ORD ? (i >> 1) + 4 * (i & 1) : i;
+            __builtin_amdgcn_raw_buffer_store_b128(val[k], rc, lane * 16, k * 1024, 2);
+        }
         if (STAGE) wsync();
     }
 }
@@ -230,35 +234,16 @@ int main(int argc, char **argv) {
         std::function<void()> fn;
     };
     std::vector<Item> items;
-    for (int m : {16, 32, 48}) {
-        const dim3 gr(cus * 4 * m);
-        const std::string x = " x" + std::to_string(m);
-        items.push_back({"rows8  stage pf" + x, [=] { hipLaunchKernelGGL((k_move<0, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"rows8  stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<0, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"flat16 stage pf" + x, [=] { hipLaunchKernelGGL((k_move<1, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"flat16 stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"flat16 regs pf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 1>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"flat16 regs nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 0>), gr, dim3(256), 0, 0, g2, flat); }});
-    }
     for (int m : {16, 32}) {
         const dim3 gr(cus * 4 * m);
         const std::string x = " x" + std::to_string(m);
-        items.push_back({"pair16 stage pf" + x, [=] { hipLaunchKernelGGL((k_move<2, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"pair16 stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<2, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"rows8  stage pf" + x, [=] { hipLaunchKernelGGL((k_move<0, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"rows8  stage pf ord1" + x, [=] { hipLaunchKernelGGL((k_move<0, 1, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"flat16 stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"flat16 stage nopf ord1" + x, [=] { hipLaunchKernelGGL((k_move<1, 1, 0, 1>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"flat16 regs nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 0>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"flat16 regs nopf ord1" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 0, 1>), gr, dim3(256), 0, 0, g2, flat); }});
     }
-    for (int o = 1; o <= 2; ++o) {
-        const Geo gg = o == 1 ? g1 : gz;
-        const std::string t = o == 1 ? " out1" : " outZ";
-        const dim3 g16(cus * 4 * 16), g32(cus * 4 * 32);
-        items.push_back({"rows8  stage pf x16" + t, [=] { hipLaunchKernelGGL((k_move<0, 1, 1>), g16, dim3(256), 0, 0, gg, flat); }});
-        items.push_back({"flat16 stage nopf x32" + t, [=] { hipLaunchKernelGGL((k_move<1, 1, 0>), g32, dim3(256), 0, 0, gg, flat); }});
-        items.push_back({"flat16 regs nopf x32" + t, [=] { hipLaunchKernelGGL((k_move<1, 0, 0>), g32, dim3(256), 0, 0, gg, flat); }});
-    }
-    int16_t *c1[2] = {(int16_t *)out1, (int16_t *)(out1 + nby * 128)};
-    int16_t *cz[2] = {(int16_t *)outZ, (int16_t *)(outZ + nby * 128)};
-    items.push_back({"fwd q50 out1", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, c1, nullptr, nullptr)); }});
-    items.push_back({"fwd q50 outZ", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, cz, nullptr, nullptr)); }});
-    items.push_back({"diag flat kind 7 -> outZ", [=] { DCHECK(dctq_diag_stream(7, src, outZ, (long long)nblk / 64 * 64, nullptr)); }});
     items.push_back({"fwd q50", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, c2, nullptr, nullptr)); }});
     items.push_back({"diag flat kind 7 (1 out)", [=] { DCHECK(dctq_diag_stream(7, src, out1, (long long)nblk / 64 * 64, nullptr)); }});
     for (int w = 0; w < 300; ++w) items[w % items.size()].fn();  // clock pre-warm
