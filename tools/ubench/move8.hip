@@ -5,7 +5,9 @@
 // One kernel template over the three differences, same bytes and buffers:
 //   LOAD  0 rows8 (8 x 8 B per lane: block rows) / 1 flat16 (4 x 16 B per lane: NOT the
 //         batch's blocks, the bytes in memory order) / 2 pair16 (16 B per lane: row 2j + h of
-//         blocks 2p, 2p + 1, transposed through the stage into lane-per-block rows, move7)
+//         blocks 2p, 2p + 1, transposed through the stage into lane-per-block rows, move7) /
+//         3 flat16 loads with pair16's LDS transpose (the instruction mix of a design that loads a
+//         contiguous block row and transposes it; the data are not blocks)
 //   STAGE 0 stores from registers (flat16 only) / 1 the product's 136-B stage
 //   PF    0 load at the loop top / 1 next batch prefetched before the stores
 // on grids of CUs x 4 x {16, 32, 48} workgroups of 4 waves, writing the outputs of two
@@ -96,7 +98,7 @@ __device__ __forceinline__ void load_batch(const Geo &g, const u4v *flat, uint32
         load_rows(g, b, lane, rows);
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = u4v{rows[2 * j].x, rows[2 * j].y, rows[2 * j + 1].x, rows[2 * j + 1].y};
-    } else if constexpr (LOAD == 1) {
+    } else if constexpr (LOAD == 1 || LOAD == 3) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = __builtin_nontemporal_load(flat + (size_t)b * 256 + j * 64 + lane);
     } else {  // pair16: lane (p, h) loads row 2j + h of blocks 2p, 2p + 1
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void k_move(Geo g, const u4v *flat) {
         } else {
             load_batch<LOAD>(g, flat, it, lane, cur);
         }
-        if constexpr (LOAD == 2) {  // rows -> LDS (row r at r * 512), then lane-per-block rows
+        if constexpr (LOAD >= 2) {  // rows -> LDS (row r at r * 512), then lane-per-block rows
             const int p = lane & 31, h = lane >> 5;
 #pragma unroll
             for (int j = 0; j < 4; ++j) *reinterpret_cast<u4v *>(ws + (2 * j + h) * 512 + p * 16) = cur[j];
@@ -238,11 +240,11 @@ int main(int argc, char **argv) {
         const dim3 gr(cus * 4 * m);
         const std::string x = " x" + std::to_string(m);
         items.push_back({"rows8  stage pf" + x, [=] { hipLaunchKernelGGL((k_move<0, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"rows8  stage pf ord1" + x, [=] { hipLaunchKernelGGL((k_move<0, 1, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"rows8  stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<0, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
         items.push_back({"flat16 stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"flat16 stage nopf ord1" + x, [=] { hipLaunchKernelGGL((k_move<1, 1, 0, 1>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"flat16 regs nopf" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 0>), gr, dim3(256), 0, 0, g2, flat); }});
-        items.push_back({"flat16 regs nopf ord1" + x, [=] { hipLaunchKernelGGL((k_move<1, 0, 0, 1>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"flat16 xpose stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<3, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"flat16 xpose stage pf" + x, [=] { hipLaunchKernelGGL((k_move<3, 1, 1>), gr, dim3(256), 0, 0, g2, flat); }});
+        items.push_back({"pair16 stage nopf" + x, [=] { hipLaunchKernelGGL((k_move<2, 1, 0>), gr, dim3(256), 0, 0, g2, flat); }});
     }
     items.push_back({"fwd q50", [=] { DCHECK(dctq_forward_quant_planes(plan, planes, 2, c2, nullptr, nullptr)); }});
     items.push_back({"diag flat kind 7 (1 out)", [=] { DCHECK(dctq_diag_stream(7, src, out1, (long long)nblk / 64 * 64, nullptr)); }});
