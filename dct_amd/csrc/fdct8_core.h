@@ -547,7 +547,7 @@ __device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict_
                                                     uint32_t &mlo, uint32_t &mhi) {
     fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
     flat_dc_fix(dev, cur, stage, lane, wv, mlo);
-    if (!valid) mlo = mhi = 0;
+    if (!valid || (DCTQ_ABLATE & 8)) mlo = mhi = 0;
 }
 
 // Phase 2 (after the prefetch fence): the batch's flagged coefficients resolved
