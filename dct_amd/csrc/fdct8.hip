@@ -523,7 +523,11 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 #define DCTQ_V3_GRID_MULT 16
 #endif
 #ifndef DCTQ_TIE_HEAVY_V3
-#define DCTQ_TIE_HEAVY_V3 0  // A/B: tie-heavy plans (DC divisor 1, q >= 97) on v3 too
+// Tie-heavy plans (DC divisor 1, q >= 97) on v3 too (round 4, session 3,
+// profiles/r04/v3_tieheavy_ab.log: against v2 at the same rotation slots, q97 -2 to -5 %,
+// q100 0 to -3 %, uniform / smooth / extreme; v3's 16x grid and pinned batch outputs
+// came after round 3's v2-favouring A/B).  v2 stays in the diagnostic library (variant 4).
+#define DCTQ_TIE_HEAVY_V3 1
 #endif
 #ifndef DCTQ_V3_LATE_FENCE
 #define DCTQ_V3_LATE_FENCE 0
@@ -622,9 +626,10 @@ int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy
     if (variant == 1) return 1;
     if (variant == 3) return 3;
     if (variant == 4) return 2;  // the queue kernel at any size (A/B)
-    // in-place ties (v3) unless the plan is tie-heavy; and always when every wave of
-    // the resident grid (16 waves per CU: 4 per SIMD, VGPR-bound) has at most one
-    // batch, where v2's end-of-kernel drain would be the whole tail
+    // in-place ties (v3) for every plan (DCTQ_TIE_HEAVY_V3; the v2 queue kernel for
+    // tie-heavy plans with it off, except when every wave of the resident grid (16 waves
+    // per CU: 4 per SIMD, VGPR-bound) has at most one batch, where v2's end-of-kernel
+    // drain would be the whole tail)
     const bool single = nbatch <= (uint32_t)(num_cus * 16);
     return single || (DCTQ_FWD_INPLACE && (!tie_heavy || DCTQ_TIE_HEAVY_V3)) ? 3 : 2;
 }

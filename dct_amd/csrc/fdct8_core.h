@@ -75,6 +75,17 @@ __device__ __forceinline__ double adaptive_scale(int32_t var_num) {
     return 2.0 - nv;
 }
 
+// out / m for the exact paths: every divisor of a tie-heavy plan is 1 (q >= 97 without
+// adaptation), and x / 1.0 == x exactly, so the fp64 division sequence (~11 VALU) runs
+// only when some lane of the wave has a divisor other than 1.
+#ifndef DCTQ_DIV_SKIP
+#define DCTQ_DIV_SKIP 1
+#endif
+__device__ __forceinline__ double exact_div(double out, double m) {
+    if (DCTQ_DIV_SKIP && !__builtin_amdgcn_ballot_w64(m != 1.0)) return out;
+    return out / m;
+}
+
 // ============================================================================
 // v2 building blocks (see fdct8.hip for the loop around them).
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -341,7 +352,7 @@ __device__ __forceinline__ int exact_from_rows(const uint2 (&rows)[8], int c, co
         const double t = row_sum(rows[k].x, rows[k].y, dj);
         out = k == 0 && DCTQ_EXACT_NOZERO ? di[0] * t : out + di[k] * t;
     }
-    return (int)round(out / m);
+    return (int)round(exact_div(out, m));
 }
 
 // Next flagged processing slot of (mlo, mhi) -> coefficient index, clearing it.
@@ -428,7 +439,7 @@ __device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c
         const double t = row_sum(rows[k].x, rows[k].y, dj);
         out = k == 0 && DCTQ_EXACT_NOZERO ? di[0] * t : out + di[k] * t;
     }
-    return (int)round(out / m);
+    return (int)round(exact_div(out, m));
 }
 
 // exact_from_rows_lds() for e <= 64 / G entries of one round, G = 8, 4 or 2 lanes
@@ -532,8 +543,9 @@ __device__ __forceinline__ uint32_t exact_grouped(const ExactTables *tab, const 
             if (m < 1.0) m = 1.0;
         }
     }
+    const double r = exact_div(out, m);
     if (part == 0 && (uint32_t)grp < e) {
-        st16[src * (kPitch2 / 2) + c] = (int16_t)(int)round(out / m);
+        st16[src * (kPitch2 / 2) + c] = (int16_t)(int)round(r);
         return 1u;
     }
     return 0u;

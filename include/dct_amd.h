@@ -42,11 +42,12 @@ typedef struct dctq_plan dctq_plan;
 
 /* quality is clamped to 1..100 exactly as quant_init does (src/quantization.c:26-31).
  * A plan holds only its ~4 KB of tables in device memory; it is reusable and
- * cheap to keep (one per quality is fine).  The forward kernel's tie-path stash
- * is the library's, one per (device, stream): allocated by the first forward
- * launch on a stream that needs it (a tie-heavy plan, q >= 97, over more 64-block
- * batches than the device has resident waves; other plans resolve their ties in
- * place), sized to that launch's grid (8 KiB per wave,
+ * cheap to keep (one per quality is fine).  Since round 4 the product forward
+ * resolves every plan's ties in place and allocates no stash; the stash below
+ * serves the tie-queue kernel (v2), which only the diagnostic library still
+ * launches.  The stash is the library's, one per (device, stream): allocated by
+ * the first v2 launch on a stream over more 64-block batches than the device has
+ * resident waves, sized to that launch's grid (8 KiB per wave,
  * at most 256 MiB on a 256-CU MI355X) and kept for later launches on the same
  * stream until dctq_stream_release.  The NULL stream and hipStreamPerThread
  * get one stash per calling thread (each thread's real stream differs).  A

@@ -89,9 +89,9 @@ def test_fastdiv(lib):
 
 def test_forward_kernel_dispatch(lib):
     """The product forward dispatch (fdct8.hip forward_kernel_for): in-place ties (v3) for
-    every plan whose DC divisor is above 1 and for launches of at most one batch per
-    resident wave; the queue kernel (v2) for tie-heavy plans (q >= 97: DC divisor 1, the
-    rational coefficients tie in ~1 block of 8) over many batches."""
+    every plan at every size.  Since round 4 that includes tie-heavy plans (q >= 97: DC
+    divisor 1, the rational coefficients tie in ~1 block of 8), which ran on the queue
+    kernel (v2) before (profiles/r04/v3_tieheavy_ab.log)."""
     import dct_amd
     big, small = 194400, 4096  # the bench step's batches; 16 waves per CU x 256 CUs
     for q in (1, 10, 50, 90, 95, 96):
@@ -99,7 +99,7 @@ def test_forward_kernel_dispatch(lib):
             assert dct_amd.forward_kernel(q, ad, big, 256).startswith("fdct8_quant_v3"), (q, ad)
     for q in (97, 99, 100):
         assert dct_amd.debug_tables(q)[3][0] <= 1.0
-        assert dct_amd.forward_kernel(q, 0, big, 256).startswith("fdct8_quant_v2"), q
+        assert dct_amd.forward_kernel(q, 0, big, 256).startswith("fdct8_quant_v3"), q
         assert dct_amd.forward_kernel(q, 0, small, 256).startswith("fdct8_quant_v3"), q
     assert dct_amd.forward_kernel(50, 1, big, 256) == "fdct8_quant_v3<true, false, false>"
 

@@ -218,8 +218,8 @@ def _adversarial_row():
 
 @pytest.mark.parametrize("variant", [4, 3, 1])
 def test_forced_kernels_adversarial_and_counter(T, dm, variant):
-    """Small launches normally run v3 (in-place ties), large ones v2 (tie queue,
-    stash, drains): each kernel forced at small sizes through the diagnostic
+    """The product runs v3 (in-place ties); v2 (tie queue, stash, drains) and v1
+    stay A/B kernels of the diagnostic library: each kernel forced at small sizes through the diagnostic
     library -- every quality on tie-prone blocks, random planes of
     every kind, and the fallback counter equal across kernels."""
     import oracle as O
@@ -255,8 +255,8 @@ def test_mid_size_tie_heavy_stream(T, dm):
     """More than 4096 64-block batches of tie-heavy content: step blocks (a quarter
     of the DCs are exact ties), 0/255 extremes and a plane whose batches alternate
     between step blocks and uniform noise, several qualities, both modes.  Through
-    the product dispatch (v3, in-place grouped passes, for every plan with DC divisor
-    > 1; v2 at q100) and with the v2 queue kernel forced (variant 4: both of its tie
+    the product dispatch (v3, in-place grouped passes, every plan since round 4) and
+    with the v2 queue kernel forced (variant 4: both of its tie
     paths, the stage and the queue, in one launch)."""
     import oracle as O
     rng = np.random.default_rng(31)
@@ -293,7 +293,8 @@ def test_plans_cheap_and_stash_per_stream(T, dm):
     stash (<= 256 MiB); the same plan on two streams at once (each stream its
     own stash) gives the oracle's coefficients on both."""
     import oracle as O
-    # 388 800 blocks: > 16 waves x 256 CUs of batches, so tie-heavy plans (q >= 97) run the v2 queue kernel
+    # 388 800 blocks: > 16 waves x 256 CUs of batches (until round 4 tie-heavy plans ran the v2 queue kernel
+    # with its stash here; every plan runs v3 now, so the product adds no stash at all)
     px = dm.synth(4242, "uniform", 3840, 2160, 3)
     outs = [T.empty((3 * 480 * 270, 64), dtype=T.int16, device="cuda") for _ in range(2)]
     T.cuda.synchronize()
@@ -303,12 +304,12 @@ def test_plans_cheap_and_stash_per_stream(T, dm):
     free1 = T.cuda.mem_get_info()[0]
     assert free0 - free1 < (1 << 30), (free0 - free1) / 2 ** 20
     side = T.cuda.Stream()
-    for p in plans[::10] + plans[96:]:  # v3 (no stash) and q97..q100 (v2: the stash)
+    for p in plans[::10] + plans[96:]:  # v3 (no stash), q97..q100 included
         p.forward_quant(px, out=outs[0])
     T.cuda.synchronize()
     free2 = T.cuda.mem_get_info()[0]
     assert free1 - free2 <= (256 << 20) + (16 << 20), (free1 - free2) / 2 ** 20
-    p = plans[98]  # q99, adaptive: v2
+    p = plans[98]  # q99, adaptive
     side.wait_stream(T.cuda.current_stream())
     p.forward_quant(px, out=outs[0])
     with T.cuda.stream(side):
