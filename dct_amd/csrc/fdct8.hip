@@ -511,7 +511,13 @@ static hipError_t launch_v2(const PlaneSet &ps, const FastTables &t, const DevTa
 #define DCTQ_V3_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>)
 #endif
 #ifndef DCTQ_V3_WIDE
-#define DCTQ_V3_WIDE 0  // resolve_ties_compact WIDE: at this kernel's 128-VGPR bound the wide rounds spill (A/B knob)
+// resolve_ties_compact WIDE for v3 without the variance output or the fallback counter:
+// passes of 9..32 entries run one round of 2 lanes per entry (round 4, session 3,
+// profiles/r04/wide2_ab.log, three rotations with every build at every slot: q97 -7 %,
+// extreme q10 -4 %, q100 -1 %, uniform q50 within the noise; the main loop's code is
+// unchanged).  The 4-lane rounds (bit 0) put a scratch reload in front of the stores, and
+// with VAR or STATS the 2-lane rounds spill too, so those instantiations keep WIDE 0.
+#define DCTQ_V3_WIDE 2
 #endif
 #ifndef DCTQ_V3_GRID_MULT
 // fdct8_quant_v3 launches 16 x its resident workgroups (round 4, profiles/r04/forward_grid_sweep.log,
@@ -579,7 +585,8 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         if (!DCTQ_V3_LATE_FENCE)
             asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                          "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-        resolved += resolve_ties_compact<ADAPTIVE, DCTQ_V3_GROUP8, DCTQ_V3_WIDE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+        resolved += resolve_ties_compact<ADAPTIVE, DCTQ_V3_GROUP8, (VAR || STATS) ? 0 : DCTQ_V3_WIDE>(
+            &tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (DCTQ_V3_LATE_FENCE)  // A/B: the tie pass while the prefetch is in flight
             asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                          "+v"(nxt[6]), "+v"(nxt[7])::"memory");
