@@ -568,7 +568,8 @@ def _tie_count_plane(rng, counts):
 def test_grouped_tie_passes(T, dm):
     """Tie passes of 0..64 entries per batch around every grouped path's bound (<= 8
     entries: 8 lanes per entry; 9..16 and 17..32 in the kernels with wide rounds, the
-    fused Huffman sizes: 4 and 2 lanes per entry; above: one entry per lane;
+    fused Huffman sizes: 4 and 2 lanes per entry, the forward without counter or variance
+    output: 2 lanes per entry for 9..32; above: one entry per lane;
     exact_grouped<G>) in every kernel that resolves ties in place -- the forward (v3;
     v2 forced beside it), the fused round trip, the encoder and the fused Huffman
     sizes -- for both modes, with the fallback counter counting every entry once."""
@@ -589,6 +590,9 @@ def test_grouped_tie_passes(T, dm):
             assert np.array_equal(got[variant], want), (ad, variant)
             assert int(cnt.item()) >= sum(counts), (ad, variant, int(cnt.item()))
         plan = dm.Plan(50, ad)
+        # without the counter: the product's v3 instantiation, whose passes of 9..32 entries run 2 lanes
+        # per entry (the counted one keeps one entry per lane: it spills with the wide rounds)
+        assert np.array_equal(plan.forward_quant(g).cpu().numpy(), want), ad
         coefs, recons = plan.round_trip_planes([g])
         assert np.array_equal(T.cat(coefs).cpu().numpy(), want), ad
         ec, off, sym = plan.encode_planes([g])
