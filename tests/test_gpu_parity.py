@@ -67,27 +67,33 @@ def test_forward_quant_full_size_digests(T, dm, digests):
 
 
 @pytest.mark.parametrize("kind,q,ad,F", [("uniform", 50, 0, 64), ("smooth", 90, 1, 16), ("const", 75, 0, 16),
-                                         ("extreme", 10, 1, 8)])
+                                         ("extreme", 10, 1, 8), ("uniform", 100, 0, 8), ("extreme", 97, 0, 8)])
 def test_bench_workload_every_block(T, dm, kind, q, ad, F):
     """The bench's own step (F 4K luma + 2F 1080p chroma planes in one dctq_forward_quant_planes launch;
     F = 64 is the headline 12 441 600 blocks with bench.py's seeds) checked block by block against the
-    oracle -- the headline number's output, not a sample of it -- plus other input kinds, qualities and the
-    adaptive mode at bench geometry, with var_num against the exact block variance numerator."""
+    oracle -- the headline number's output, not a sample of it -- plus other input kinds, qualities (tie-heavy
+    q97 / q100 included) and the adaptive mode at bench geometry.  Twice: as the bench launches it (no
+    variance output: the kernel instantiation the bench times, with its 2-lane tie rounds) and with var_num,
+    checked against the exact block variance numerator."""
     import oracle as O
     luma = dm.synth(12345, kind, 3840, 2160, F)
     chroma = dm.synth(12345 + 50000, kind, 1920, 1080, 2 * F)
     ny, nc = F * 480 * 270, 2 * F * 240 * 135
     vy = T.empty(ny, dtype=T.int32, device="cuda")
     vc = T.empty(nc, dtype=T.int32, device="cuda")
-    cy, cc = dm.Plan(q, ad).forward_quant_planes([luma, chroma], var_nums=[vy, vc])
+    plan = dm.Plan(q, ad)
+    by, bc = plan.forward_quant_planes([luma, chroma])
+    cy, cc = plan.forward_quant_planes([luma, chroma], var_nums=[vy, vc])
     threads = min(16, os.cpu_count() or 1)
-    for px, coef, vn, per in ((luma, cy, vy, 480 * 270), (chroma, cc, vc, 240 * 135)):
+    for px, bench_c, coef, vn, per in ((luma, by, cy, vy, 480 * 270), (chroma, bc, cc, vc, 240 * 135)):
         host_px = px.cpu().numpy()
+        host_b = bench_c.cpu().numpy()
         host_c = coef.cpu().numpy()
         host_v = vn.cpu().numpy()
         for f in range(px.shape[0]):
             want = O.forward_plane(host_px[f], q, ad, threads)
-            assert np.array_equal(host_c[f * per:(f + 1) * per], want), f"{kind}: frame {f} of {tuple(px.shape)}"
+            assert np.array_equal(host_b[f * per:(f + 1) * per], want), f"{kind}: frame {f} of {tuple(px.shape)}"
+            assert np.array_equal(host_c[f * per:(f + 1) * per], want), f"{kind} +var: frame {f} of {tuple(px.shape)}"
         wv = O.plane_variance(host_px[-1]) * 4096.0  # var_num / 4096 == calculate_block_variance exactly
         assert np.array_equal(host_v[-per:].astype(np.float64), wv), kind
 
