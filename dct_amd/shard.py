@@ -100,10 +100,11 @@ def gather_p2p(locals_, counts, group=None):
         full[offs[rank]:offs[rank + 1]].copy_(src)
         for d in range(1, world):  # peers in ring order from this rank: every link busy at once
             to, frm = (rank + d) % world, (rank - d) % world
+            # group_peer: ranks within `group` (a subgroup's rank r is not global rank r)
             if c[rank]:
-                ops.append(dist.P2POp(dist.isend, _wire(src), to, group))
+                ops.append(dist.P2POp(dist.isend, _wire(src), group=group, group_peer=to))
             if c[frm]:
-                ops.append(dist.P2POp(dist.irecv, _wire(full[offs[frm]:offs[frm + 1]]), frm, group))
+                ops.append(dist.P2POp(dist.irecv, _wire(full[offs[frm]:offs[frm + 1]]), group=group, group_peer=frm))
         fulls.append(full)
     if ops:
         for w in dist.batch_isend_irecv(ops):

@@ -78,6 +78,21 @@ def _worker(rank, world, port, q):
         with pytest.raises(ValueError):
             shard.gather_coefficients(local, counts, method="ring")
 
+        # (2d) both shapes inside a SUBGROUP that excludes global rank 0: its ranks are not the
+        # global ones, so the direct pushes must address peers by group rank
+        sub_ranks = list(range(1, world)) if world > 2 else [0, 1]
+        sub = dist.new_group(sub_ranks)  # collective over the world: every rank calls it
+        if rank in sub_ranks:
+            sw, sr = len(sub_ranks), sub_ranks.index(rank)
+            mine, (lo, hi) = shard.frame_shard(frames, sw, sr)
+            local = torch.from_numpy(np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in mine])
+                                     if hi > lo else np.zeros((0, 64), np.int16))
+            counts = [(shard.split(5, sw, r)[1] - shard.split(5, sw, r)[0]) * 30 for r in range(sw)]
+            for method in shard.GATHER_METHODS:
+                full = shard.gather_coefficients(local, counts, group=sub, method=method)
+                assert np.array_equal(full.numpy(), want), f"subgroup gather differs ({method})"
+        dist.barrier()
+
         # (3) run-length streams of the frame shards (what dctq_encode_planes makes on each GPU)
         mine, (lo, hi) = shard.frame_shard(frames, world, rank)
         local = (np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in mine])
