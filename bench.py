@@ -73,6 +73,10 @@ def parse():
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
     ap.add_argument("--total-frames", type=int, default=64,
                     help="N>1 gather leg (BASELINE configs[3]): 4K luma frames in total, split over the ranks")
+    ap.add_argument("--gather-fault", default="none", choices=["none", "offset"],
+                    help="tests only: 'offset' makes every rank transform the frames one past its own slice (a "
+                         "wrong shard offset shared by both gather shapes), so the gather leg's "
+                         "gathered_equals_unsharded must read false")
     ap.add_argument("--encode-steps", type=int, default=10,
                     help="timed steps of the encoder leg (forward + zigzag/RLE symbols; at N>1 plus the "
                          "symbol-stream all-gather); 0 = skip")
@@ -402,7 +406,10 @@ def gather_leg(args, plan, world, rank, dev):
     from dct_amd import shard
     lo, hi = shard.split(args.total_frames, world, rank)
     per = (Y_W // 8) * (Y_H // 8)
-    frames = dct_amd.synth(args.seed + 200000 + lo, args.kind, Y_W, Y_H, max(hi - lo, 1), device=dev)[:hi - lo]
+    # frame f of synth(seed, n) is made from seed + f, so seeding by the global index of the
+    # shard's first frame makes the shards tile the unsharded stack exactly
+    first = (lo + 1) % args.total_frames if args.gather_fault == "offset" else lo
+    frames = dct_amd.synth(args.seed + 200000 + first, args.kind, Y_W, Y_H, max(hi - lo, 1), device=dev)[:hi - lo]
     out = torch.empty(((hi - lo) * per, 64), dtype=torch.int16, device=dev)
     counts = [(b - a) * per for a, b in (shard.split(args.total_frames, world, r) for r in range(world))]
 
@@ -411,7 +418,17 @@ def gather_leg(args, plan, world, rank, dev):
             plan.forward_quant(fr, out=out)
         return out
 
-    r = shard.strong_gather_leg(forward, frames, counts, args.gather_steps, dev, torch.cuda.synchronize)
+    def unsharded(chunk=8):
+        """The unsharded forward of all --total-frames frames, recomputed on this rank
+        chunk by chunk (8 frames at a time): what every rank must hold after a gather."""
+        buf = torch.empty((chunk, Y_H, Y_W), dtype=torch.uint8, device=dev)
+        for g0 in range(0, args.total_frames, chunk):
+            n = min(chunk, args.total_frames - g0)
+            fr = dct_amd.synth(args.seed + 200000 + g0, args.kind, Y_W, Y_H, n, device=dev, out=buf[:n])
+            yield g0 * per, plan.forward_quant(fr)
+
+    r = shard.strong_gather_leg(forward, frames, counts, args.gather_steps, dev, torch.cuda.synchronize,
+                                unsharded=unsharded)
     local = r["local"]
     off = sum(counts[:rank])
     n = r["blocks_per_step"] * r["steps"]
@@ -419,18 +436,23 @@ def gather_leg(args, plan, world, rank, dev):
     by = {m: {"op": gather_op_name(m), "blocks_per_s": n / v["end_to_end_s"],
               "ms_per_step": v["end_to_end_s"] / r["steps"] * 1e3,
               "own_slice_intact": bool(torch.equal(v["full"][off:off + counts[rank]], local)),
+              "gathered_equals_unsharded": v["gathered_equals_unsharded"],
               "xgmi": shard.xgmi_report(recv, v["gather_s"] / r["steps"], world)}
           for m, v in r["by_method"].items()}
     full0 = r["full"]
     same = all(bool(torch.equal(v["full"], full0)) for v in r["by_method"].values())
-    first = by[shard.GATHER_METHODS[0]]
-    return {"op": f"{args.total_frames} 4K luma frames split over {world} ranks: forward_quant + {first['op']} of the "
-                  "int16 coefficient planes (BASELINE configs[3])", "scaling": "strong", "world_size": world,
+    # every rank checked its own copy: the leg passes only if all of them hold the unsharded result
+    ok = torch.tensor([int(all(v["gathered_equals_unsharded"] for v in by.values()))], device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    first_m = by[shard.GATHER_METHODS[0]]
+    return {"op": f"{args.total_frames} 4K luma frames split over {world} ranks: forward_quant + {first_m['op']} of "
+                  "the int16 coefficient planes (BASELINE configs[3])", "scaling": "strong", "world_size": world,
             "frames_total": args.total_frames, "frames_this_rank": hi - lo, "steps": r["steps"],
             "kernel_blocks_per_s": n / r["kernel_s"], "kernel_ms_per_step": r["kernel_s"] / r["steps"] * 1e3,
-            "blocks_per_s": first["blocks_per_s"], "ms_per_step": first["ms_per_step"],
+            "blocks_per_s": first_m["blocks_per_s"], "ms_per_step": first_m["ms_per_step"],
             "bytes_received_per_rank": recv, "own_slice_intact": all(v["own_slice_intact"] for v in by.values()),
-            "methods_gather_the_same": same, "xgmi": first["xgmi"], "methods": by}
+            "methods_gather_the_same": same, "gathered_equals_unsharded": bool(ok.item()),
+            "fault_injected": args.gather_fault, "xgmi": first_m["xgmi"], "methods": by}
 
 
 def small_frame_leg(args, plan, dev):
@@ -671,7 +693,13 @@ def round_trip_leg(args, plan, luma, chroma, world, rank, dev):
     (_,), (r_other,) = other.round_trip_planes([luma[0]])
     psnr_other = psnr_of(r_other)
     bpb = 64 + 128 + 256
+    inv_bound, inv_f32 = dct_amd.inverse_bound(args.quality, args.adaptive)
     return {"op": "round_trip_planes (fused forward+inverse, one launch per step; BASELINE configs[4])",
+            "kernel": "roundtrip8_f32" if inv_f32 else "roundtrip8",
+            "inverse": {"arithmetic": "fp32" if inv_f32 else "fp64",
+                        "error_bound": inv_bound if inv_f32 else None,
+                        "rule": "fp32 when the rigorous bound of tools/inv_bound.py for this plan is <= 5e-5 "
+                                "(non-adaptive plans; q <= 71 of the standard table), else the paired fp64 inverse"},
             "world_size": world, "scaling": "weak", "frames_per_gpu": luma.shape[0], "steps": args.round_trip_steps,
             "blocks_per_s": world * nblk * args.round_trip_steps / el,
             "ms_per_step": el / args.round_trip_steps * 1e3,

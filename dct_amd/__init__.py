@@ -63,6 +63,8 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
         sig.update({
             "dctq_diag_plan_set_variant": ([vp, i], i),
             "dctq_diag_plan_set_num_cus": ([vp, i], i),
+            "dctq_diag_plan_set_inverse": ([vp, i], i),
+            "dctq_debug_inverse_bound": ([i, i, C.POINTER(i)], C.c_double),
             "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_movement_v2_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_movement_grid_planes": ([vp, C.POINTER(_Plane), i, vp, i, vp], i),
@@ -165,15 +167,18 @@ class Plan:
     (quant_init(8, quality, adaptive) semantics, src/quantization.c:19-41)."""
 
     def __init__(self, quality: int = 50, adaptive: bool = False, variant: int = None, diagnostic: bool = False,
-                 num_cus: int = None):
+                 num_cus: int = None, inverse: str = None):
         """variant (tests / A/B only): force the forward kernel through the diagnostic
         library (dctq_diag_plan_set_variant: 1 = v1, 3 = v3 in-place ties, 4 = v2 tie
         queue, at any size); num_cus (tests only): launch as if the device had that many
         CUs (dctq_diag_plan_set_num_cus: smaller grids, more batches per wave);
         diagnostic: create the plan in the diagnostic library (needed for
-        diag_movement_planes)."""
+        diag_movement_planes); inverse="fp64" (tests only): the fused round trip uses
+        the paired-lane fp64 inverse even when the plan is admitted to the fp32 one
+        (dctq_diag_plan_set_inverse)."""
         self.quality, self.adaptive = quality, bool(adaptive)
-        self._L = diag() if (variant is not None or num_cus is not None or diagnostic) else lib()
+        diagnostic = diagnostic or variant is not None or num_cus is not None or inverse is not None
+        self._L = diag() if diagnostic else lib()
         h = C.c_void_p()
         self._chk(self._L.dctq_plan_create(int(quality), int(bool(adaptive)), C.byref(h)))
         self._h = h
@@ -181,6 +186,10 @@ class Plan:
             self._chk(self._L.dctq_diag_plan_set_variant(h, int(variant)))
         if num_cus is not None:
             self._chk(self._L.dctq_diag_plan_set_num_cus(h, int(num_cus)))
+        if inverse is not None:
+            if inverse not in ("fp64", "auto"):
+                raise DctqError('inverse must be "fp64" or "auto"')
+            self._chk(self._L.dctq_diag_plan_set_inverse(h, 0 if inverse == "fp64" else 1))
 
     def _chk(self, rc: int) -> None:
         _check(rc, self._L)
@@ -421,6 +430,15 @@ def forward_kernel(quality: int, adaptive: bool, batches: int, num_cus: int) -> 
     `batches` 64-block batches on num_cus CUs (host-only, dctq_debug_forward_kernel)."""
     v = diag().dctq_debug_forward_kernel(int(quality), int(bool(adaptive)), int(batches), int(num_cus))
     return f"fdct8_quant_v{v}<{str(bool(adaptive)).lower()}, false, false>"
+
+
+def inverse_bound(quality: int, adaptive: bool = False):
+    """Host-only: (bound, admitted) -- the rigorous bound of |recon - reference| of the
+    fused round trip's fp32 inverse for this standard-table plan, and whether
+    round_trip_planes runs that inverse for it (tools/inv_bound.py, api.hip)."""
+    a = C.c_int(0)
+    b = diag().dctq_debug_inverse_bound(int(quality), int(bool(adaptive)), C.byref(a))
+    return float(b), bool(a.value)
 
 
 def debug_tables(quality: int, adaptive: bool = False):

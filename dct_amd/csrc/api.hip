@@ -23,6 +23,7 @@
 #include "dctq_internal.h"
 #include "fdct8_bound.h"
 #include "host_tables.h"
+#include "idct8_bound.h"
 #include "plan.h"
 
 namespace {
@@ -101,6 +102,40 @@ void dctq::dc_const_table(const double *d, const double *q, int16_t *tab) {
     }
 }
 
+// The fused round trip's fp32 inverse is admitted for a non-adaptive plan when the
+// rigorous bound of tools/inv_bound.py (idct8_bound.h) keeps |recon - reference|
+// within kInvTol (5e-5, half of north_star's 1e-4) for EVERY input block:
+// |c_uv| <= 128 L1(D_u) L1(D_v) for centred pixels, so |q_uv| <= round(c_max / Q)
+// and |x_uv| <= B_uv = |q|max * (1/Q) * S_u S_v (the reference's 1/Q dequantisation,
+// src/quantization.c:139,144); per output pixel the bound is G.B (1 + u) + u (128 + |L|.B)
+// (the final + 128 rounding) + 1e-9 (the reference's own fp64 error).
+static_assert(kInvTol == kInvTolDiag, "plan.h's copy of the fp32 inverse's admission tolerance");
+double dctq::inverse_f32_bound(const dctq::DevTables &t) {
+    const double u = 1.0 / 16777216.0;
+    double l1[8];
+    for (int r = 0; r < 8; ++r) {
+        l1[r] = 0.0;
+        for (int c = 0; c < 8; ++c) l1[r] += fabs(t.dct[r * 8 + c]);
+    }
+    double B[64];
+    for (int k = 0; k < 64; ++k) {
+        const double cmax = 128.0 * l1[k >> 3] * l1[k & 7] * (1.0 + 1e-12);
+        const double qmax = floor(cmax / t.quant[k] + 0.5 + 1e-9);
+        B[k] = qmax * t.dequant[k] * t.s2[k] * (1.0 + 1e-12);
+    }
+    double worst = 0.0;
+    for (int p = 0; p < 64; ++p) {
+        double g = 0.0, a = 0.0;
+        for (int k = 0; k < 64; ++k) {
+            g += kInvErrG[p][k] * B[k];
+            a += kInvAbsL[p][k] * B[k];
+        }
+        const double e = g * (1.0 + u) + u * (128.0 + a) + 1e-9;
+        worst = e > worst ? e : worst;
+    }
+    return worst;
+}
+
 static int build_plan(const double *q, int quality, int adaptive, dctq_plan **out) {
     if (!out) return fail(DCTQ_EINVAL, "plan pointer is NULL");
     for (int c = 0; c < 64; ++c)
@@ -130,6 +165,9 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
     dctq::fill_fast_tables(q, p->adaptive, &p->fast);
     dctq::dc_const_table(p->host.dct, p->host.quant, p->host.dc_const);
     for (int k = 0; k < 8; ++k) p->host.s1[k] = kAanScale[k];
+    for (int c = 0; c < 64; ++c) p->host.iscale32[c] = (float)p->host.iscale[c];
+    p->inv_bound = dctq::inverse_f32_bound(p->host);
+    p->inv_f32 = !p->adaptive && p->inv_bound <= kInvTol;
     p->host.fast = p->fast;
     hipError_t e = hipMalloc(&p->dev, sizeof(dctq::DevTables));
     if (e != hipSuccess) {
@@ -411,7 +449,8 @@ int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int 
         if (!recon[k] || ((uintptr_t)recon[k]) % 16) return fail(DCTQ_EINVAL, "recon[k] NULL or not 16-byte aligned");
         rt.recon[k] = recon[k];
     }
-    HIPCHK(dctq::launch_roundtrip(rt, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream, plan->num_cus),
+    HIPCHK(dctq::launch_roundtrip(rt, plan->dev, plan->adaptive, plan->inv_f32 != 0, plan->fallbacks,
+                                  (hipStream_t)stream, plan->num_cus),
            "roundtrip launch");
     return DCTQ_OK;
 }

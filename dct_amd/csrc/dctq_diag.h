@@ -19,6 +19,11 @@ extern "C" {
  * dctq_forward_float / dctq_inverse to their lane-per-block kernels when 1. */
 int dctq_diag_plan_set_variant(dctq_plan *plan, int variant);
 
+/* The fused round trip's inverse (test-only): mode 0 forces the paired-lane fp64
+ * inverse; 1 restores the plan's own choice (the fp32 inverse when the plan is
+ * admitted by the rigorous bound of tools/inv_bound.py, see dctq_debug_inverse_bound). */
+int dctq_diag_plan_set_inverse(dctq_plan *plan, int mode);
+
 /* Launch every kernel of a plan as if the device had num_cus CUs (1..4096; the
  * grids are capped per CU), so a test-sized input gives each wave many batches
  * (test-only: on the full grid a wave of the fused Huffman kernel sees about one
@@ -74,6 +79,10 @@ int dctq_debug_forward_kernel(int quality, int adaptive, long long batches, int 
 int dctq_debug_tables(int quality, int adaptive, float *w, float *thr, double *dct, double *quant);
 int dctq_debug_dc_table(int quality, int16_t *out);
 int dctq_debug_fastdiv(uint32_t d, uint32_t n);
+/* The rigorous bound of |recon - reference| of the round trip's fp32 inverse for a
+ * standard-table plan (api.hip inverse_f32_bound); *admitted = whether
+ * dctq_round_trip_planes runs that inverse for it (non-adaptive, bound <= 5e-5). */
+double dctq_debug_inverse_bound(int quality, int adaptive, int *admitted);
 
 #ifdef __cplusplus
 }

@@ -78,6 +78,7 @@ struct DevTables {
     double qscale[64]; // inverse path (adaptive): Q * S_i S_j
     double s2[64];     // S_i S_j
     double s1[8];      // S_k: AAN output scale X_k = S_k y_k (per-slot factors of the paired fp64 kernels)
+    float iscale32[64];// fl32(iscale): the fused round trip's fp32 inverse (plans admitted by idct8_bound.h)
     FastTables fast;   // device copy of the fast-path tables (v2 reads them per batch)
     // quantized DC of a CONSTANT block of centred value v-128, computed on the
     // host in the reference's order (src/dct.c:57-74, src/quantization.c:124):
@@ -139,8 +140,9 @@ size_t fdct8_ring_bytes(int workgroups);
 // shape 3: fdct8_movement, 2: fdct8_movement_v2; grid_mult 0 = the product kernel's grid
 hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape,
                                  int grid_mult = 0);
-hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
-                            hipStream_t stream, int num_cus);
+// inv_f32: the plan is admitted to the fp32 inverse (api.hip, tools/inv_bound.py); otherwise the paired fp64 one
+hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, bool inv_f32,
+                            unsigned long long *fallbacks, hipStream_t stream, int num_cus);
 // diagnostic: roundtrip8's data movement without arithmetic (roundtrip.hip)
 hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream, int num_cus);
 size_t encode_workspace_bytes(long long nbatch);

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include "dctq_diag.h"
+#include "fdct8_bound.h"
 #include "host_tables.h"
 #include "plan.h"
 
@@ -92,6 +93,27 @@ int dctq_diag_plan_set_variant(dctq_plan *plan, int variant) {
     if (variant < 1 || variant > 4) return dctq::fail(DCTQ_EINVAL, "variant must be 1..4");
     plan->variant = variant;
     return DCTQ_OK;
+}
+
+int dctq_diag_plan_set_inverse(dctq_plan *plan, int mode) {
+    DCTQ_ENTRY;
+    if (!plan) return dctq::fail(DCTQ_EINVAL, "plan is NULL");
+    if (mode != 0 && mode != 1) return dctq::fail(DCTQ_EINVAL, "mode must be 0 (fp64) or 1 (the plan's own choice)");
+    plan->inv_f32 = mode == 1 && !plan->adaptive && plan->inv_bound <= kInvTolDiag;
+    return DCTQ_OK;
+}
+
+double dctq_debug_inverse_bound(int quality, int adaptive, int *admitted) {
+    dctq::DevTables t;
+    dctq_host::dct_matrix(8, t.dct);
+    dctq_host::quant_matrix(8, dctq_host::clamp_quality(quality), t.quant);
+    for (int c = 0; c < 64; ++c) {
+        t.dequant[c] = 1.0 / t.quant[c];
+        t.s2[c] = kAanScale[c >> 3] * kAanScale[c & 7];
+    }
+    const double b = dctq::inverse_f32_bound(t);
+    if (admitted) *admitted = !adaptive && b <= kInvTolDiag;
+    return b;
 }
 
 int dctq_diag_plan_set_num_cus(dctq_plan *plan, int num_cus) {

@@ -13,6 +13,8 @@ struct dctq_plan {
     dctq::DevTables host;        // host copy of the device tables
     dctq::DevTables *dev;        // device copy
     unsigned long long *fallbacks;
+    int inv_f32;                 // round trip: fp32 inverse admitted (|recon err| <= inv_bound <= kInvTol)
+    double inv_bound;            // the fp32 inverse's rigorous error bound for this plan (idct8_bound.h)
 };
 
 namespace dctq {
@@ -27,6 +29,13 @@ int plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef, int32
 void fill_fast_tables(const double *q, int adaptive, FastTables *t);
 // quantized DC of every constant block, in the reference's operation order (api.hip)
 void dc_const_table(const double *d, const double *q, int16_t *tab);
+// rigorous bound of |recon - reference| of the fused round trip's fp32 inverse for the
+// plan's tables (non-adaptive dequantisation; tools/inv_bound.py, idct8_bound.h)
+double inverse_f32_bound(const DevTables &t);
+}  // namespace dctq
+// the admission tolerance of that bound (== idct8_bound.h kInvTol; api.hip checks they agree)
+constexpr double kInvTolDiag = 5e-5;
+namespace dctq {
 }  // namespace dctq
 
 #define HIPCHK(call, what)                                               \

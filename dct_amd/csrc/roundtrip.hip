@@ -100,6 +100,202 @@ __device__ __forceinline__ void inverse_half(const DevTables *__restrict__ dev, 
     }
 }
 
+// The 8-point transposed AAN graph in fp32, operation for operation
+// tools/aan_model.py aan8t (the graph tools/inv_bound.py bounds; aan8t_d in fp64),
+// with the fp32 constants of fdct8_bound.h.  Every op is a separately rounded fp32
+// add / sub / mul or an explicit fma (-ffp-contract=off).
+__device__ __forceinline__ void aan8t_f(float &v0, float &v1, float &v2, float &v3, float &v4, float &v5, float &v6,
+                                        float &v7) {
+    const float gz13 = v5 + v3, gz2 = v5 - v3, gz11 = v1 + v7, gz4 = v1 - v7;
+    float gb0 = gz11 + gz13;
+    const float gz3 = gz11 - gz13;
+    const float go1 = gz3 * DCTQ_C4;
+    const float gz5 = (gz2 + gz4) * DCTQ_C6;
+    const float go0 = __builtin_fmaf(DCTQ_C2MC6, gz2, gz5);
+    const float go2 = __builtin_fmaf(DCTQ_C2PC6, gz4, -gz5);
+    const float gb3 = go0, gb2 = go0 + go1, gb1 = go1 + go2;
+    gb0 = gb0 + go2;
+    float ge3 = v2 + v6;
+    const float gm = v2 - v6;
+    const float gs = gm * DCTQ_C4;
+    const float ge2 = gs;
+    ge3 = ge3 + gs;
+    const float ge0 = v0 + v4, ge1 = v0 - v4;
+    const float ga0 = ge0 + ge3, ga3 = ge0 - ge3, ga1 = ge1 + ge2, ga2 = ge1 - ge2;
+    v0 = ga0 + gb0;
+    v1 = ga1 + gb1;
+    v2 = ga2 + gb2;
+    v3 = ga3 + gb3;
+    v4 = ga3 - gb3;
+    v5 = ga2 - gb2;
+    v6 = ga1 - gb1;
+    v7 = ga0 - gb0;
+}
+
+// Dequantize + inverse DCT + 128 of the lane's own block in fp32, for the plans
+// api.hip admits (inverse_f32_bound: |recon - reference| <= 5e-5 for every input
+// block; non-adaptive only, whose dequantisation is the reference's q * (1/Q),
+// src/quantization.c:139,144): x_uv = fl32(q_uv * fl32(iscale_uv)) (one v_pk_mul per
+// coefficient pair, the scale pair in SGPRs), the columns then the rows through
+// aan8t_f (src/dct.c:80-105 as D^T X D), then + 128 (tools/inv_bound.py models
+// exactly this sequence).  qw = the block's 64 int16 (row-major, two per dword).
+__device__ __forceinline__ void inverse_block_f32(const DevTables *__restrict__ dev, const uint2 (&qw)[16],
+                                                  float (&x)[64]) {
+    ConstTables *tp = tables(dev);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t w[2] = {qw[r].x, qw[r].y};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = 4 * r + 2 * h;
+            const f2 q = {(float)(int)(int16_t)(w[h] & 0xFFFFu), (float)((int)w[h] >> 16)};
+            const f2 sc = {tp->iscale32[c], tp->iscale32[c + 1]};
+            const f2 v = q * sc;
+            x[c] = v.x;
+            x[c + 1] = v.y;
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < 8; ++v)
+        aan8t_f(x[v], x[8 + v], x[16 + v], x[24 + v], x[32 + v], x[40 + v], x[48 + v], x[56 + v]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        aan8t_f(x[8 * i], x[8 * i + 1], x[8 * i + 2], x[8 * i + 3], x[8 * i + 4], x[8 * i + 5], x[8 * i + 6],
+                x[8 * i + 7]);
+    const f2 k128 = {128.0f, 128.0f};
+#pragma unroll
+    for (int c = 0; c < 64; c += 2) {
+        const f2 v = f2{x[c], x[c + 1]} + k128;
+        x[c] = v.x;
+        x[c + 1] = v.y;
+    }
+}
+
+// The 8 KiB recon half of the wave's stage (32 blocks at kPitchP, as store_stage
+// reads it) into registers, and those registers to HBM: store_stage in two steps,
+// so a caller can keep one half's store data live while it reads the next.
+__device__ __forceinline__ void stage_read_half(const uint4 *stage, int wv, int lane, u4p (&val)[8]) {
+    const char *base = reinterpret_cast<const char *>(stage) + wv * 32 * kPitchP;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint4 t = *reinterpret_cast<const uint4 *>(base + (4 * k + (lane >> 4)) * kPitchP + (lane & 15) * 16);
+        val[k] = u4p{t.x, t.y, t.z, t.w};
+    }
+}
+__device__ __forceinline__ void store_half(const u4p (&val)[8], int lane, char *dst, uint32_t nbytes) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nbytes, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
+}
+
+// Lane l writes its block's 256 B of recon at the stage slot (l & 31) -- the
+// blocks of the batch's first 32 lanes (HALF 0) or of its last 32 (HALF 1).
+template <int HALF>
+__device__ __forceinline__ void stage_recon_half(char *wstage, int lane, const float (&x)[64]) {
+    if ((lane >> 5) == HALF) {
+        float4 *dst = reinterpret_cast<float4 *>(wstage + (lane & 31) * kPitchP);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[r] = make_float4(x[4 * r], x[4 * r + 1], x[4 * r + 2], x[4 * r + 3]);
+    }
+}
+
+// The fused round trip with the fp32 inverse (non-adaptive plans admitted by
+// api.hip inverse_f32_bound, e.g. q <= 71 of the standard table).  Phases 1-2 are
+// roundtrip8's; phase 3 runs lane per block (no transposes, half the fp64 kernel's
+// VALU issue: PMC profiles/r05/): every lane inverts its own block in registers,
+// then the recon leaves through the stage in two 8 KiB halves (blocks 0-31, then
+// 32-63).  The second half's read-back lands in registers disjoint from the first
+// half's pending store data (kept live across it), so no vmcnt(0) sits between the
+// two halves' stores; the only waits are the prefetch fence after the forward and
+// one retire of the coefficient stores after the inverse, both behind a compute phase.
+template <bool VAR, bool STATS>
+__global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8_f32(RoundTripSet rt,
+                                                                       const DevTables *__restrict__ dev,
+                                                                       unsigned long long *fallbacks) {
+    __shared__ uint4 stage[kThreads * kPitch2 / 16];
+    __shared__ ExactTables tab;
+    __shared__ uint16_t scr[kWaves * 64];  // resolve_ties_compact's entries
+    load_exact_tables(&tab, dev);
+    const PlaneSet &ps = rt.ps;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nbatch = ps.first[ps.n];
+    const uint32_t step = gridDim.x * kWaves;
+    uint32_t g = blockIdx.x * kWaves + wv;
+    uint2 nxt[8];
+    prefetch_batch(ps, g, lane, nxt);
+    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
+                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
+    uint32_t exact_count = 0;
+    char *wstage = reinterpret_cast<char *>(stage) + wv * 64 * kPitch2;
+    for (; g < nbatch; g += step) {
+        const int k = plane_of(ps, g);
+        const PlaneArgs &p = ps.pl[k];
+        const uint32_t b = g - first_of(ps, k);
+        uint2 cur[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
+        const bool valid = b * 64 + lane < (uint32_t)p.nblk;
+        prefetch_batch<false>(ps, g + step, lane, nxt);
+        const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
+        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
+        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
+
+        // ---- 1. forward into the stage; ties resolved in place
+        int32_t var_num;
+        uint32_t mlo, mhi;
+        forward_flags_batch<false, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
+        retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
+        const uint32_t ne = resolve_ties_compact<false, true, 0>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+        if (STATS) exact_count += ne;
+        wave_sync();
+
+        // ---- 2. read-back: the coefficient chunks and the lane's own block
+        const uint32_t nb = out.nb;
+        u4v val[8];
+        stage_chunks(stage, wv, lane, val);
+        uint2 qw[16];
+        {
+            const uint2 *row = reinterpret_cast<const uint2 *>(wstage + lane * kPitch2);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) qw[r] = row[r];
+        }
+        {
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
+            if (VAR) {
+                const __amdgpu_buffer_rsrc_t rv =
+                    __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(nb * 4u), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_NT_AUX);
+            }
+        }
+
+        // ---- 3. fp32 inverse, lane per block; recon out in two 8 KiB halves
+        float x[64];
+        inverse_block_f32(dev, qw, x);
+        stage_recon_half<0>(wstage, lane, x);
+        retire_stores();  // the coefficient stores have read their data (store-data hazard)
+        wave_sync();
+        u4p va[8], vb[8];
+        stage_read_half(stage, wv, lane, va);
+        store_half(va, lane, recon, (nb < 32u ? nb : 32u) * 256u);
+        stage_recon_half<1>(wstage, lane, x);
+        wave_sync();
+        stage_read_half(stage, wv, lane, vb);
+        // A's store data stays live until B's rows are in: B's LDS loads cannot land in it
+#pragma unroll
+        for (int c = 0; c < 8; ++c) asm volatile("" : "+v"(vb[c]) : "v"(va[c]));
+        store_half(vb, lane, recon + 32 * 256, (nb > 32u ? nb - 32u : 0u) * 256u);
+    }
+    if (STATS) {
+        uint32_t tot = exact_count;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+        if (lane == 0 && tot) atomicAdd(fallbacks, (unsigned long long)tot);
+    }
+}
+
 template <bool ADAPTIVE, bool VAR, bool STATS>
 __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet rt, const DevTables *__restrict__ dev,
                                                           unsigned long long *fallbacks) {
@@ -207,15 +403,23 @@ static hipError_t launch_rt(const RoundTripSet &rt, const DevTables *dev, unsign
 }
 
 // ============================================================================
-// Diagnostic: roundtrip8's data movement with no arithmetic -- the memory
-// ceiling of this exact access pattern (bench.py round_trip.movement_ceiling).
-// Same grid, occupancy bound, LDS footprint, prefetch, retire/sync points and
-// stores as roundtrip8: per batch the pixel rows go into the stage as the
-// "coefficients" (8 x 1 KiB stores), then twice 32 blocks of 256 B "recon"
-// (the rows repeated) through the paired-inverse stage layout (8 x 1 KiB each).
+// Diagnostic: the data movement of roundtrip8_f32 (the kernel the bench's plan
+// runs) with no arithmetic -- the memory ceiling of that access pattern (bench.py
+// round_trip.movement_ceiling).  Same grid, occupancy bound, LDS footprint,
+// prefetch, stage writes, LDS read-backs and stores: per batch the pixel rows go
+// into the stage as the "coefficients" (8 x 1 KiB stores), then each lane's row
+// read-back, repeated, is its block's 256 B of "recon" (two halves of 8 x 1 KiB).
+// No wait is placed where the product waits behind a compute phase: a vmcnt(0)
+// with no arithmetic in front of it stalls on the memory the product overlaps
+// (round 4's version waited on its own prefetch at once and ran 6.5 % SLOWER than
+// the product: VERDICT r04).  The only waits are the ones the compiler inserts for
+// the prefetched rows before their use.  Without the retires, a read-back may land
+// in registers an older store still reads (the store-data hazard of DESIGN.md 3.1):
+// that can change the bytes this diagnostic writes, never where it writes them
+// (the buffer offsets stay live, and num_records clips every store).
 __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(RoundTripSet rt) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ ExactTables tabpad;          // same LDS footprint as roundtrip8
+    __shared__ ExactTables tabpad;          // same LDS footprint as roundtrip8_f32
     __shared__ uint16_t scrpad[kWaves * 64];
     const PlaneSet &ps = rt.ps;
     if (ps.n < 0) {  // keep the padding allocated
@@ -223,7 +427,6 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(Roun
         reinterpret_cast<volatile uint32_t *>(&tabpad)[threadIdx.x] = 0;
     }
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int h = lane >> 5, j = lane & 31;
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kWaves;
     uint32_t g = blockIdx.x * kWaves + wv;
@@ -243,7 +446,6 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(Roun
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
         uint2 *mine2 = reinterpret_cast<uint2 *>(wstage + lane * kPitch2);
-        retire_stores();
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             mine2[2 * r] = cur[r];
@@ -253,26 +455,32 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(Roun
         const uint32_t nb = out.nb;
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
+        uint2 qw[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) qw[r] = mine2[r];
         {
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
 #pragma unroll
             for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
         }
-        char *mine = wstage + j * kPitchP + h * 128;
+        float x[64];
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            retire_stores();
-            wave_sync();
-#pragma unroll
-            for (int r = 0; r < 8; ++r)
-                *reinterpret_cast<uint4 *>(mine + r * 16) =
-                    make_uint4(cur[r].x, cur[r].y, cur[r].x ^ (uint32_t)half, cur[r].y ^ (uint32_t)lane);
-            retire_stores();
-            wave_sync();
-            const uint32_t n32 = half ? (nb > 32u ? nb - 32u : 0u) : (nb < 32u ? nb : 32u);
-            store_stage(stage, wv, lane, recon + half * 32 * 256, n32 * 256u);
+        for (int r = 0; r < 32; ++r) {
+            x[2 * r] = __uint_as_float(qw[r & 15].x);
+            x[2 * r + 1] = __uint_as_float(qw[r & 15].y);
         }
+        stage_recon_half<0>(wstage, lane, x);
+        wave_sync();
+        u4p va[8], vb[8];
+        stage_read_half(stage, wv, lane, va);
+        store_half(va, lane, recon, (nb < 32u ? nb : 32u) * 256u);
+        stage_recon_half<1>(wstage, lane, x);
+        wave_sync();
+        stage_read_half(stage, wv, lane, vb);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) asm volatile("" : "+v"(vb[c]) : "v"(va[c]));
+        store_half(vb, lane, recon + 32 * 256, (nb > 32u ? nb - 32u : 0u) * 256u);
     }
 }
 
@@ -285,9 +493,26 @@ hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream,
     return hipGetLastError();
 }
 
-hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
-                            hipStream_t stream, int num_cus) {
+template <bool V, bool S>
+static hipError_t launch_rt_f32(const RoundTripSet &rt, const DevTables *dev, unsigned long long *fb,
+                                hipStream_t stream, int num_cus) {
+    static const int per_cu = resident_per_cu(roundtrip8_f32<V, S>, kThreads);
+    const uint32_t nbatch = rt.ps.first[rt.ps.n];
+    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_RT_GRID_MULT);
+    hipLaunchKernelGGL((roundtrip8_f32<V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt, dev, fb);
+    return hipGetLastError();
+}
+
+hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, bool inv_f32,
+                            unsigned long long *fallbacks, hipStream_t stream, int num_cus) {
     const bool a = adaptive != 0, v = rt.ps.var[0] != nullptr, s = fallbacks != nullptr;
+    if (inv_f32 && !a) {
+        if (v) return s ? launch_rt_f32<true, true>(rt, dev, fallbacks, stream, num_cus)
+                        : launch_rt_f32<true, false>(rt, dev, fallbacks, stream, num_cus);
+        return s ? launch_rt_f32<false, true>(rt, dev, fallbacks, stream, num_cus)
+                 : launch_rt_f32<false, false>(rt, dev, fallbacks, stream, num_cus);
+    }
     if (a) {
         if (v) return s ? launch_rt<true, true, true>(rt, dev, fallbacks, stream, num_cus)
                         : launch_rt<true, true, false>(rt, dev, fallbacks, stream, num_cus);

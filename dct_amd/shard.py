@@ -259,8 +259,26 @@ def max_over_ranks(seconds: float, device, group=None) -> float:
     return float(t.item())
 
 
+def equals_unsharded(full, chunks) -> bool:
+    """Whether a gathered [sum(counts), ...] tensor equals the unsharded result,
+    given as `chunks`: an iterable of (first_block, expected) pieces that tile
+    the whole output in order (each rank recomputes them locally, so a wrong peer
+    offset or rank order that every gather shape shares is caught -- comparing
+    the shapes with each other, or a rank's own slice, would not).  Pieces are
+    compared as they come, so the full expected tensor never exists at once."""
+    import torch
+    end = 0
+    for first, want in chunks:
+        if first != end or first + want.shape[0] > full.shape[0]:
+            return False
+        if not torch.equal(full[first:first + want.shape[0]], want.to(full.device)):
+            return False
+        end = first + want.shape[0]
+    return end == full.shape[0]
+
+
 def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: None, group=None,
-                      methods=GATHER_METHODS) -> dict:
+                      methods=GATHER_METHODS, unsharded=None) -> dict:
     """BASELINE configs[3]: a fixed batch of frames split over the ranks
     (strong scaling; `frames` is this rank's frame_shard), forward DCT+quant of
     the shard, then the coefficient planes gathered onto every rank.
@@ -278,7 +296,10 @@ def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: 
                     exchange alone, for its achieved bytes per second per rank.
     Returns the times (the first method's under the plain keys, every method's
     under by_method[m]), the blocks per step and the last gathered tensor of
-    each method (full = the first method's)."""
+    each method (full = the first method's).  With `unsharded` (a callable
+    returning equals_unsharded's chunks of the unsharded forward, recomputed on
+    this rank), every method's gathered tensor is checked against it:
+    by_method[m]["gathered_equals_unsharded"]."""
     import time
     import torch.distributed as dist
     total = sum(counts)
@@ -302,6 +323,8 @@ def strong_gather_leg(forward, frames, counts, steps: int, device, sync=lambda: 
         t_e2e, full = timed(lambda: gather_coefficients(forward(frames), counts, group, m))
         t_gather, _ = timed(lambda: gather_coefficients(local, counts, group, m))
         by[m] = {"end_to_end_s": t_e2e, "gather_s": t_gather, "full": full}
+        if unsharded is not None:
+            by[m]["gathered_equals_unsharded"] = equals_unsharded(full, unsharded())
     first = by[methods[0]]
     return {"blocks_per_step": total, "steps": steps, "kernel_s": t_kernel, "end_to_end_s": first["end_to_end_s"],
             "gather_s": first["gather_s"], "local": local, "full": first["full"], "by_method": by}

@@ -443,6 +443,18 @@ def test_bench_gpus2_gloo(T, dm):
     assert g["methods_gather_the_same"] is True and g["methods"]["p2p"]["own_slice_intact"] is True, g
     assert b["methods"]["p2p"]["gathered_equals_unsharded"] is True, b
     assert g["methods"]["p2p"]["xgmi"]["bytes_received_per_rank"] == g["bytes_received_per_rank"], g
+    # the gather leg checks each shape's result against the unsharded forward, every rank
+    assert g["gathered_equals_unsharded"] is True and g["fault_injected"] == "none", g
+    for m in ("all_gather", "p2p"):
+        assert g["methods"][m]["gathered_equals_unsharded"] is True, (m, g)
+    # ... and a wrong shard offset shared by both shapes fails it (both shapes still agree)
+    cmd_f = cmd + ["--gather-fault", "offset", "--round-trip-steps", "0", "--encode-steps", "0"]
+    r = subprocess.run(cmd_f, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    g = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])["gather"]
+    assert g["fault_injected"] == "offset" and g["methods_gather_the_same"] is True, g
+    assert g["gathered_equals_unsharded"] is False, g
+    assert not any(g["methods"][m]["gathered_equals_unsharded"] for m in ("all_gather", "p2p")), g
 
 
 def test_dist_legs_rccl_one_rank(T, dm):
@@ -738,9 +750,11 @@ def test_round_trip_planes_fused(T, dm):
                 err = np.abs(r.cpu().numpy().astype(np.float64) - want_r).max()
                 assert err <= 1e-4, (q, ad, p.shape, err)
                 assert np.array_equal(r.cpu().numpy(), r2.cpu().numpy())
-                # and the same floats as the unfused dctq_inverse
+                # and the unfused dctq_inverse's floats (fp64 arithmetic: half an fp32 ulp from
+                # the reference), within the fused kernel's own bound when it runs the fp32 inverse
                 ri = plan.inverse(c, var_num=v).cpu().numpy()
-                assert np.abs(ri - r.cpu().numpy()).max() <= 2e-5
+                bound, f32 = dm.inverse_bound(q, ad)
+                assert np.abs(ri - r.cpu().numpy()).max() <= (bound + 2e-5 if f32 else 2e-5), (q, ad, f32)
 
 
 @pytest.mark.parametrize("ad", [0, 1])
@@ -783,6 +797,57 @@ def test_round_trip_full_size_4k420(T, dm, ad):
     assert abs(psnr_gpu - psnr_ref) <= 1e-3, (psnr_gpu, psnr_ref)
     # the bug-compatible 1/Q dequantization gives ~11 dB on noise, adaptive ~23 dB
     assert (psnr_ref < 15.0) if ad == 0 else (psnr_ref > 15.0), psnr_ref
+
+
+def _basis_sign_blocks():
+    """For every (u, v), the u8 block whose centred pixels are +-127/-128 with the signs
+    of D[u][i] D[v][j], and its negation: each maximises |c_uv| (the bound's
+    |c_uv| <= 128 L1(D_u) L1(D_v)), so its quantized coefficient and dequantized
+    input to the inverse are as large as the plan allows.  A 8 x 1024 plane."""
+    import oracle as O
+    D = O.dct_matrix(8)
+    blocks = []
+    for u in range(8):
+        for v in range(8):
+            sg = np.where(np.outer(D[u], D[v]) >= 0, 1, -1)
+            blocks += [128 + 127 * sg, 128 - 128 * sg]
+    b = np.clip(np.array(blocks), 0, 255).astype(np.uint8)  # [128, 8, 8]
+    return np.ascontiguousarray(b.transpose(1, 0, 2).reshape(8, 128 * 8))
+
+
+def test_round_trip_inverse_fp32_within_bound(T, dm):
+    """The fused round trip's fp32 inverse (roundtrip8_f32): a non-adaptive plan runs
+    it only when the rigorous bound of tools/inv_bound.py (api.hip
+    inverse_f32_bound) keeps |recon - reference| <= 5e-5 for every input block
+    (q <= 71 of the standard table).  On blocks that maximise each coefficient, noise,
+    extremes, flat and smooth planes: coefficients bit-exact in both inverses, the
+    fp32 inverse within its plan's bound (<= 1e-4, north_star), the forced fp64
+    inverse within half an fp32 ulp of the reference (src/dct.c:80-105,
+    src/quantization.c:133-151), and plans past the bound run the fp64 inverse."""
+    import oracle as O
+    planes = [_basis_sign_blocks(), O.synth_plane(3, O.KINDS["extreme"], 256, 64),
+              O.synth_plane(4, O.KINDS["uniform"], 256, 64), O.synth_plane(5, O.KINDS["const"], 128, 64),
+              O.synth_plane(6, O.KINDS["smooth"], 128, 64)]
+    for q in (1, 10, 50, 71, 72, 90):
+        bound, admitted = dm.inverse_bound(q, 0)
+        assert admitted == (q <= 71) and admitted == (bound <= 5e-5), (q, bound)
+        assert dm.inverse_bound(q, 1)[1] is False  # adaptive plans keep the fp64 inverse
+        p_auto, p64 = dm.Plan(q, 0), dm.Plan(q, 0, inverse="fp64")
+        for px in planes:
+            g = gpu_px(T, px)
+            (c,), (r,) = p_auto.round_trip_planes([g])
+            (c2,), (r2,) = p64.round_trip_planes([g])
+            want_c = O.forward_plane(px, q, 0)
+            assert np.array_equal(c.cpu().numpy(), want_c) and np.array_equal(c2.cpu().numpy(), want_c), q
+            want_r = O.inverse_plane(want_c, q, 0) + 128.0
+            got, got64 = r.cpu().numpy(), r2.cpu().numpy()
+            half_ulp = np.spacing(np.abs(want_r).astype(np.float32)).astype(np.float64) / 2
+            assert (np.abs(got64.astype(np.float64) - want_r) <= half_ulp + 1e-9).all(), q
+            e32 = float(np.abs(got.astype(np.float64) - want_r).max())
+            if admitted:
+                assert e32 <= bound <= 1e-4, (q, px.shape, e32, bound)
+            else:
+                assert np.array_equal(got, got64), q
 
 
 def test_round_trip_exact_count_matches_forward(T, dm):

@@ -116,7 +116,22 @@ def _worker(rank, world, port, q):
             return torch.from_numpy(np.concatenate([O.forward_plane(f.numpy(), 75, 0) for f in fr])
                                     if fr.shape[0] else np.zeros((0, 64), np.int16))
 
-        r = shard.strong_gather_leg(forward, stack[lo:hi], counts, 2, torch.device("cpu"))
+        def unsharded():  # the whole stack's forward, recomputed here, in two pieces
+            w = np.concatenate([O.forward_plane(f.numpy(), 75, 0) for f in stack])
+            return [(0, torch.from_numpy(w[:5])), (5, torch.from_numpy(w[5:]))]
+
+        r = shard.strong_gather_leg(forward, stack[lo:hi], counts, 2, torch.device("cpu"), unsharded=unsharded)
+        for m, rm in r["by_method"].items():
+            assert rm["gathered_equals_unsharded"] is True, m
+        # a wrong shard offset shared by both gather shapes (every rank transforms the frames
+        # one past its own slice): both shapes still agree with each other, the unsharded
+        # check catches it on every rank
+        shifted = stack[[(f + 1) % total for f in range(lo, hi)]]
+        bad = shard.strong_gather_leg(forward, shifted, counts, 1, torch.device("cpu"), unsharded=unsharded)
+        assert torch.equal(bad["by_method"]["p2p"]["full"], bad["by_method"]["all_gather"]["full"])
+        assert not any(v["gathered_equals_unsharded"] for v in bad["by_method"].values()), rank
+        assert not shard.equals_unsharded(torch.zeros(4, 64, dtype=torch.int16),
+                                          [(0, torch.zeros(2, 64, dtype=torch.int16))])  # short cover
         assert r["blocks_per_step"] == total * per and r["steps"] == 2
         assert r["kernel_s"] > 0 and r["end_to_end_s"] > 0 and r["gather_s"] > 0
         assert set(r["by_method"]) == set(shard.GATHER_METHODS)

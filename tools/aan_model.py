@@ -43,6 +43,7 @@ class Exact:
     def sub(self, a, b): return a - b
     def mul(self, a, k): return a * k
     def fma(self, k, a, b): return k * a + b
+    def neg(self, a): return -a
 
 
 def scales():
@@ -61,3 +62,26 @@ def scales():
 
 if __name__ == "__main__":
     print(scales())
+
+
+def aan8t(v, A):
+    """The transposed flow graph A^T (dct_amd/csrc/aan_f64.h aan8t_d and the fp32
+    inverse of roundtrip.hip, operation for operation): with D = diag(S) A
+    orthonormal, D^T X = A^T (S .* X).  fma(K, a, b) = K*a + b."""
+    gz13, gz2 = A.add(v[5], v[3]), A.sub(v[5], v[3])
+    gz11, gz4 = A.add(v[1], v[7]), A.sub(v[1], v[7])
+    gb0, gz3 = A.add(gz11, gz13), A.sub(gz11, gz13)
+    go1 = A.mul(gz3, C4)
+    gz5 = A.mul(A.add(gz2, gz4), C6)
+    go0 = A.fma(C2mC6, gz2, gz5)
+    go2 = A.fma(C2pC6, gz4, A.neg(gz5))
+    gb3, gb2, gb1 = go0, A.add(go0, go1), A.add(go1, go2)
+    gb0 = A.add(gb0, go2)
+    ge3, gm = A.add(v[2], v[6]), A.sub(v[2], v[6])
+    gs = A.mul(gm, C4)
+    ge2 = gs
+    ge3 = A.add(ge3, gs)
+    ge0, ge1 = A.add(v[0], v[4]), A.sub(v[0], v[4])
+    ga0, ga3, ga1, ga2 = A.add(ge0, ge3), A.sub(ge0, ge3), A.add(ge1, ge2), A.sub(ge1, ge2)
+    return [A.add(ga0, gb0), A.add(ga1, gb1), A.add(ga2, gb2), A.add(ga3, gb3),
+            A.sub(ga3, gb3), A.sub(ga2, gb2), A.sub(ga1, gb1), A.sub(ga0, gb0)]
