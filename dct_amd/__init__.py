@@ -70,6 +70,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
             "dctq_diag_movement_grid_planes": ([vp, C.POINTER(_Plane), i, vp, i, vp], i),
             "dctq_diag_rt_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
             "dctq_diag_stream": ([i, vp, vp, ll, vp], i),
+            "dctq_diag_stream_release": ([vp], i),
             "dctq_debug_tables": ([i, i, vp, vp, vp, vp], i),
             "dctq_debug_fastdiv": ([C.c_uint32, C.c_uint32], i),
             "dctq_debug_dc_table": ([i, vp], i),
@@ -362,11 +363,13 @@ class Plan:
 
 
 def stream_release(stream=None, diagnostic: bool = False) -> None:
-    """dctq_stream_release: wait for `stream` (torch's current one by default) and
-    free the forward's tie-path stashes this thread's launches on it hold (the
-    library that ran them: diagnostic=True for plans of libdct_amd_diag.so)."""
+    """diagnostic=True: dctq_diag_stream_release -- wait for `stream` (torch's current
+    one by default) and free the tie-path stashes this thread's v2 (variant 4)
+    launches on it hold.  The product's dctq_stream_release is a no-op (it keeps no
+    per-stream memory)."""
     L = diag() if diagnostic else lib()
-    _check(L.dctq_stream_release(_stream_ptr(stream)), L)
+    fn = L.dctq_diag_stream_release if diagnostic else L.dctq_stream_release
+    _check(fn(_stream_ptr(stream)), L)
 
 
 def rle_encode(coef, stream=None):

@@ -26,7 +26,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libdct_amd.so")
 DIAG_LIB = os.path.join(HERE, "libdct_amd_diag.so")
-DIAG_SOURCES = ["diag.hip"]
+DIAG_SOURCES = ["diag.hip", "fdct8_diag.hip"]
 SOURCES = ["api.hip", "legacy.hip", "fdct8.hip", "fdct8_aux.hip", "f64_pair.hip", "rle.hip", "roundtrip.hip", "encode.hip", "huffman.hip"]
 HEADERS = ["dctq_internal.h", "plan.h", "dctq_diag.h", "fdct8_bound.h", "idct8_bound.h", "host_tables.h", "aan_f64.h", "fdct8_core.h", "pair_core.h", "scan_core.h", "zigzag.h"]
 ARCH = "gfx950"

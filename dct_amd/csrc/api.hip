@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -41,6 +42,8 @@ int fail(int code, const char *what, hipError_t e) {
 }
 }  // namespace dctq
 using dctq::fail;
+
+dctq::DiagKernels dctq::g_diag_kernels = {};  // filled by fdct8_diag.hip in libdct_amd_diag.so only
 
 namespace dctq {
 FastDiv make_fastdiv(uint32_t d) {
@@ -231,6 +234,34 @@ RandIsolation::~RandIsolation() {
     if (--g_rand_depth == 0) setstate(saved_);
     g_rand_mu.unlock();
 }
+
+namespace {
+std::atomic<bool> g_runtime_up{false};  // some launch entry point initialised the HIP runtime
+struct SeenKey {
+    int device;
+    const void *stream;
+    uint32_t entries;  // bit e: entry point e already called by this thread on (device, stream)
+};
+}  // namespace
+
+LaunchIsolation::LaunchIsolation(const void *stream, int entry) {
+    thread_local std::vector<SeenKey> seen;
+    const uint32_t bit = 1u << (entry & 31);
+    int dev = -1;
+    if (g_runtime_up.load(std::memory_order_acquire) && hipGetDevice(&dev) == hipSuccess) {
+        for (SeenKey &k : seen)
+            if (k.device == dev && k.stream == stream && (k.entries & bit)) return;  // steady state: no lock
+    }
+    iso_.emplace();
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return;  // the call itself reports the error
+    g_runtime_up.store(true, std::memory_order_release);
+    for (SeenKey &k : seen)
+        if (k.device == dev && k.stream == stream) {
+            k.entries |= bit;
+            return;
+        }
+    seen.push_back(SeenKey{dev, stream, bit});
+}
 }  // namespace dctq
 
 extern "C" {
@@ -310,107 +341,13 @@ int dctq::plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef,
     return DCTQ_OK;
 }
 
-// The v2 forward's tie-path pixel stash (fdct8.hip: 8 KiB per wave of the
-// launched grid).  One per (device, stream), allocated on the first launch that
-// needs it and grown to the largest grid launched there: launches on one stream
-// run in order, so every plan used on that stream shares it, and a plan costs
-// no stash at all until it runs a multi-batch-per-wave forward.  The mutex is
-// held from the lookup to the kernel launch (stash_guard), so a grow -- which
-// waits for the stream before freeing the smaller stash -- never frees memory a
-// launch enqueued by another thread is about to use.
-//  * The special handles name a different real stream per thread
-//    (hipStreamPerThread always; the null stream under per-thread default-stream
-//    semantics, which a caller may have compiled with): they are keyed by the
-//    calling thread too, so two threads never share a stash through them.
-//  * A launch captured into a graph gets a stash of its OWN, never shared with
-//    direct launches or other captures and never freed by a grow: a replay may
-//    run at any later time, on any stream.  It is allocated in relaxed capture
-//    mode (no stream work) and released by dctq_stream_release.
-namespace {
-struct Stash {
-    void *ptr = nullptr;
-    size_t bytes = 0;
-};
-struct StreamStash {
-    Stash live;                   // direct launches on this stream
-    std::vector<void *> captured;  // one per captured launch, kept until dctq_stream_release
-};
-struct StashKey {
-    int device;
-    hipStream_t stream;
-    std::thread::id thread;  // default-constructed (no thread) for ordinary streams
-    bool operator<(const StashKey &o) const {
-        if (device != o.device) return device < o.device;
-        if (stream != o.stream) return std::less<hipStream_t>()(stream, o.stream);
-        return thread < o.thread;
-    }
-};
-std::mutex g_stash_mu;
-std::map<StashKey, StreamStash> g_stash;
-struct StashCtx {
-    int device;
-    hipStream_t stream;
-    hipError_t err;
-};
-
-StashKey stash_key(int device, hipStream_t stream) {
-    const bool per_thread = stream == nullptr || stream == hipStreamPerThread;
-    return StashKey{device, stream, per_thread ? std::this_thread::get_id() : std::thread::id()};
-}
-
-void *stash_for(void *vctx, size_t bytes) {  // called with g_stash_mu held
-    StashCtx &c = *static_cast<StashCtx *>(vctx);
-    StreamStash &s = g_stash[stash_key(c.device, c.stream)];
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(c.stream, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone) {
-        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-        (void)hipThreadExchangeStreamCaptureMode(&mode);
-        void *p = nullptr;
-        c.err = hipMalloc(&p, bytes);
-        (void)hipThreadExchangeStreamCaptureMode(&mode);  // restore the caller's mode
-        if (c.err != hipSuccess) return nullptr;
-        s.captured.push_back(p);
-        return p;
-    }
-    if (s.live.bytes >= bytes) return s.live.ptr;
-    if (s.live.ptr) {
-        if ((c.err = hipStreamSynchronize(c.stream)) != hipSuccess) return nullptr;
-        (void)hipFree(s.live.ptr);
-        s.live = Stash{};
-    }
-    if ((c.err = hipMalloc(&s.live.ptr, bytes)) != hipSuccess) {
-        s.live = Stash{};
-        return nullptr;
-    }
-    s.live.bytes = bytes;
-    return s.live.ptr;
-}
-}  // namespace
-
 extern "C" {
 
+// The library holds no per-stream memory since round 5 (the tie-queue kernel and its
+// pixel stash are the diagnostic library's, fdct8_diag.hip): kept for ABI compatibility.
 int dctq_stream_release(void *stream) {
-    DCTQ_ENTRY;
-    int dev = -1;
-    HIPCHK(hipGetDevice(&dev), "hipGetDevice");
-    std::lock_guard<std::mutex> stash_guard(g_stash_mu);
-    auto it = g_stash.find(stash_key(dev, (hipStream_t)stream));
-    if (it == g_stash.end()) return DCTQ_OK;
-    HIPCHK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
-    (void)hipFree(it->second.live.ptr);
-    for (void *p : it->second.captured) (void)hipFree(p);
-    g_stash.erase(it);
+    (void)stream;
     return DCTQ_OK;
-}
-
-long long dctq_diag_stream_stash_bytes(void *stream) {
-    DCTQ_ENTRY;
-    int dev = -1;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::lock_guard<std::mutex> stash_guard(g_stash_mu);
-    auto it = g_stash.find(stash_key(dev, (hipStream_t)stream));
-    if (it == g_stash.end()) return 0;
-    return (long long)it->second.live.bytes;
 }
 
 }  // extern "C"
@@ -419,27 +356,24 @@ extern "C" {
 
 int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                               int32_t *const *var_num, void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 0);
     if (int rc = dctq::check_plan(plan)) return rc;
     dctq::PlaneSet ps;
     int rc = dctq::plane_set(planes, nplanes, coef, var_num, &ps);
     if (rc) return rc;
-    StashCtx sc{plan->device, (hipStream_t)stream, hipSuccess};
-    hipError_t e;
-    {
-        std::lock_guard<std::mutex> stash_guard(g_stash_mu);
-        e = dctq::launch_fdct8_quant(ps, plan->fast, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
-                                     plan->variant, plan->num_cus, dctq::RingSource{stash_for, &sc},
-                                     plan->host.quant[0] <= 1.0);  // the same test as dctq_debug_forward_kernel
+    if (plan->variant == 1 || plan->variant == 4) {  // diagnostic plans only (dctq_diag_plan_set_variant)
+        if (!dctq::g_diag_kernels.forward_quant) return fail(DCTQ_EINVAL, "forward variant not in this library");
+        return dctq::g_diag_kernels.forward_quant(plan, ps, (hipStream_t)stream);
     }
-    if (sc.err != hipSuccess) return fail(DCTQ_ENOMEM, "tie-path stash", sc.err);
-    HIPCHK(e, "fdct8_quant launch");
+    HIPCHK(dctq::launch_fdct8_quant(ps, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
+                                    plan->num_cus),
+           "fdct8_quant_v3 launch");
     return DCTQ_OK;
 }
 
 int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                            int32_t *const *var_num, float *const *recon, void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 1);
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!recon) return fail(DCTQ_EINVAL, "recon is NULL");
     dctq::RoundTripSet rt = {};
@@ -462,7 +396,7 @@ size_t dctq_encode_workspace_bytes(long long total_blocks) {
 int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
                        uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
                        void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 2);
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!offsets || !workspace) return fail(DCTQ_EINVAL, "offsets/workspace is NULL");
     if (symbols_capacity < 0) return fail(DCTQ_EINVAL, "symbols_capacity < 0");
@@ -484,21 +418,20 @@ int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int npla
 }
 
 int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num, void *stream) {
-    DCTQ_ENTRY;
     if (!src) return fail(DCTQ_EINVAL, "plane is NULL");
     return dctq_forward_quant_planes(plan, src, 1, &coef, var_num ? &var_num : nullptr, stream);
 }
 
 int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 3);
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!coef) return fail(DCTQ_EINVAL, "coef is NULL");
     if (((uintptr_t)coef) % 16) return fail(DCTQ_EINVAL, "coef must be 16-byte aligned");
     dctq::PlaneArgs a;
     int rc = dctq::plane_args(src, &a);
     if (rc) return rc;
-    if (plan->variant == 1)
-        HIPCHK(dctq::launch_fdct8_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
+    if (plan->variant == 1 && dctq::g_diag_kernels.forward_float)  // diagnostic plans only
+        HIPCHK(dctq::g_diag_kernels.forward_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
     else
         HIPCHK(dctq::launch_fdct8_float_pair(a, plan->dev, coef, (hipStream_t)stream, plan->num_cus),
                "fdct8_float_pair launch");
@@ -507,15 +440,16 @@ int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef
 
 int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks, float *recon,
                  void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 4);
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!coef || !recon) return fail(DCTQ_EINVAL, "coef/recon is NULL");
     if (plan->adaptive && !var_num) return fail(DCTQ_EINVAL, "adaptive inverse needs var_num");
     if (nblocks < 0 || nblocks >= (1ll << 40)) return fail(DCTQ_EINVAL, "bad nblocks");
     if (((uintptr_t)coef) % 16 || ((uintptr_t)recon) % 16) return fail(DCTQ_EINVAL, "coef/recon must be 16-byte aligned");
     if (nblocks == 0) return DCTQ_OK;
-    if (plan->variant == 1)
-        HIPCHK(dctq::launch_idct8(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream),
+    if (plan->variant == 1 && dctq::g_diag_kernels.inverse)  // diagnostic plans only
+        HIPCHK(dctq::g_diag_kernels.inverse(plan->dev, plan->adaptive, coef, var_num, nblocks, recon,
+                                            (hipStream_t)stream),
                "idct8 launch");
     else
         HIPCHK(dctq::launch_idct8_pair(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream,
@@ -525,7 +459,7 @@ int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_
 }
 
 int dctq_synth(uint64_t seed, int kind, const dctq_plane *dst, void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 5);
     if (!dst || !dst->pixels) return fail(DCTQ_EINVAL, "dst is NULL");
     if (dst->width <= 0 || dst->height <= 0 || dst->width % 4 || dst->stride < dst->width || dst->stride % 4 ||
         dst->nframes < 1 || ((uintptr_t)dst->pixels) % 4)
@@ -552,7 +486,7 @@ static int rle_args(const void *a, const void *b, long long nblocks) {
 size_t dctq_rle_workspace_bytes(long long nblocks) { return dctq::rle_workspace_bytes(nblocks < 1 ? 1 : nblocks); }
 
 int dctq_rle_count(const int16_t *coef, long long nblocks, uint32_t *offsets, void *workspace, void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 6);
     if (int rc = rle_args(coef, offsets, nblocks)) return rc;
     if (!workspace) return fail(DCTQ_EINVAL, "workspace is NULL");
     HIPCHK(dctq::launch_rle_count(coef, nblocks, offsets, workspace, (hipStream_t)stream, device_cus()),
@@ -561,7 +495,7 @@ int dctq_rle_count(const int16_t *coef, long long nblocks, uint32_t *offsets, vo
 }
 
 int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offsets, uint32_t *symbols, void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 7);
     if (int rc = rle_args(coef, offsets, nblocks)) return rc;
     if (!symbols) return fail(DCTQ_EINVAL, "symbols is NULL");
     HIPCHK(dctq::launch_rle_emit(coef, nblocks, offsets, symbols, ~0ull, (hipStream_t)stream, device_cus()),
@@ -571,7 +505,7 @@ int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offset
 
 int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
                     void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 8);
     if (int rc = rle_args(symbols, offsets, nblocks)) return rc;
     if (!coef) return fail(DCTQ_EINVAL, "coef is NULL");
     HIPCHK(dctq::launch_rle_decode(symbols, offsets, nblocks, coef, (hipStream_t)stream, device_cus()),
@@ -580,7 +514,7 @@ int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long 
 }
 
 int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 9);
     if (!coef || !bits) return fail(DCTQ_EINVAL, "coef/bits is NULL");
     if (nblocks < 0) return fail(DCTQ_EINVAL, "nblocks < 0");
     if (((uintptr_t)coef) % 16 || ((uintptr_t)bits) % 4) return fail(DCTQ_EINVAL, "coef must be 16-byte, bits 4-byte aligned");
@@ -591,7 +525,7 @@ int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, vo
 
 int dctq_huffman_bits_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *bits,
                              void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 10);
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!bits || ((uintptr_t)bits) % 4) return fail(DCTQ_EINVAL, "bits is NULL or not 4-byte aligned");
     // pixel planes only: the coefficients stay on chip (es.ps.coef stays NULL)
@@ -641,7 +575,7 @@ int dctq_memcpy_dtoh(void *dst, const void *src, size_t bytes) {
     return DCTQ_OK;
 }
 int dctq_synchronize(void *stream) {
-    DCTQ_ENTRY;
+    DCTQ_LAUNCH(stream, 11);
     HIPCHK(hipStreamSynchronize((hipStream_t)stream), "hipStreamSynchronize");
     return DCTQ_OK;
 }

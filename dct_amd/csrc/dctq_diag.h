@@ -67,8 +67,13 @@ int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes
  * both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
 
-/* Bytes of the tie-path stash the calling thread's launches on `stream` use for
- * direct (uncaptured) forward launches; 0 if none (tests of dctq_stream_release). */
+/* The v2 queue kernel (variant 4) keeps a tie-path pixel stash per (device,
+ * stream[, thread for the NULL stream and hipStreamPerThread]), sized to its grid;
+ * a launch captured into a graph gets one of its own.  Release waits for `stream`
+ * and frees the calling thread's stashes on it (direct and captured: call it only
+ * after the last replay of such a graph); DCTQ_EINVAL while `stream` is being
+ * captured.  Bytes: the stash direct launches on `stream` use (0 if none). */
+int dctq_diag_stream_release(void *stream);
 long long dctq_diag_stream_stash_bytes(void *stream);
 
 /* Host-only introspection for the CPU tests (no GPU needed). */

@@ -3,15 +3,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <optional>
+
 namespace dctq {
 
 // The HSA runtime calls srand()/rand() (libhsa-runtime64 imports both), which
 // would reseed or advance the HOST APPLICATION's rand() stream; the reference's
 // own tests draw their blocks from rand() (tests/test_quantization.c:127,134).
-// Every exported entry point holds one of these while it may reach the HIP
-// runtime: glibc's global random state is swapped to a private one for the
-// duration (initstate/setstate keep the caller's state and position intact).
-// Entry points are serialised by it (recursive, so nesting is fine).
+// The entry points that allocate or free device memory or set up devices (plan
+// create / destroy, the device-memory helpers, the legacy per-block API, the
+// diagnostic library) hold one of these while they may reach the HIP runtime:
+// glibc's global random state is swapped to a private one for the duration
+// (initstate/setstate keep the caller's state and position intact).  Those entry
+// points are serialised by it (recursive, so nesting is fine); the batched launch
+// entry points are not (LaunchIsolation below).
 class RandIsolation {
   public:
     RandIsolation();
@@ -23,6 +28,25 @@ class RandIsolation {
     char *saved_;
 };
 #define DCTQ_ENTRY ::dctq::RandIsolation dctq_rand_isolation_
+
+// The batched launch entry points (and dctq_synchronize) do NOT serialise: the
+// runtime's one rand() user (srand(now); rand() inside libhsa-runtime64, reached
+// when the runtime initialises or creates device resources -- a stream's first
+// hardware queue, a module's first load) can only run on a thread's FIRST call of
+// an entry point on a stream, so that call is isolated as above; every later call
+// of the thread with the same (device, stream, entry point) takes no lock and
+// touches no global state (the reference API is reentrant and keeps
+// no mutable global state).  `entry` < 32 names the entry point.
+class LaunchIsolation {
+  public:
+    LaunchIsolation(const void *stream, int entry);
+    LaunchIsolation(const LaunchIsolation &) = delete;
+    LaunchIsolation &operator=(const LaunchIsolation &) = delete;
+
+  private:
+    std::optional<RandIsolation> iso_;
+};
+#define DCTQ_LAUNCH(stream, entry) ::dctq::LaunchIsolation dctq_launch_isolation_((stream), (entry))
 
 
 // Resident workgroups per CU of `kernel` at `threads` per workgroup (>= 1).  The
@@ -119,31 +143,20 @@ struct RoundTripSet {
     float *recon[kMaxPlanes];
 };
 
-// Where the v2 forward gets its tie-path pixel stash: get(ctx, bytes) returns
-// device memory of at least `bytes` that no other in-flight launch uses, or
-// nullptr (api.hip: one stash per (device, stream), grown to the launched grid).
-struct RingSource {
-    void *(*get)(void *ctx, size_t bytes);
-    void *ctx;
-};
-// tie_heavy: the plan's DC divisor is 1 (q >= 97): the rational coefficients tie in
-// ~1 block of 8, and the product dispatch keeps the queue kernel (v2) for it.
-hipError_t launch_fdct8_quant(const PlaneSet &ps, const FastTables &t, const DevTables *dev, int adaptive,
-                              unsigned long long *fallbacks, hipStream_t stream, int variant, int num_cus,
-                              const RingSource &ring, bool tie_heavy);
-// the forward kernel (1, 2 or 3 = fdct8_quant_v1/v2/v3) launch_fdct8_quant runs
+// The product forward (fdct8.hip): fdct8_quant_v3 over every plane of ps, every plan.
+hipError_t launch_fdct8_quant(const PlaneSet &ps, const DevTables *dev, int adaptive, unsigned long long *fallbacks,
+                              hipStream_t stream, int num_cus);
+// diagnostic library (fdct8_diag.hip): the forward kernel (1, 2 or 3 = fdct8_quant_v1/v2/v3)
+// a plan of `variant` runs (the product: 3 for every plan and size)
 int forward_kernel_for(int variant, uint32_t nbatch, int num_cus, bool tie_heavy);
-// bytes of the v2 tie-path pixel stash for a grid of `workgroups` (64 B per queue slot)
-size_t fdct8_ring_bytes(int workgroups);
-// diagnostic: the forward's data movement without arithmetic (fdct8.hip): shape 3 =
-// fdct8_quant_v3's (the product kernel), 2 = fdct8_quant_v2's (the tie-heavy plans' queue kernel)
-// shape 3: fdct8_movement, 2: fdct8_movement_v2; grid_mult 0 = the product kernel's grid
+// diagnostic: the forward's data movement without arithmetic (fdct8_diag.hip): shape 3 =
+// fdct8_quant_v3's (the product kernel), 2 = fdct8_quant_v2's (the queue kernel);
+// grid_mult 0 = the product kernel's grid
 hipError_t launch_fdct8_movement(const PlaneSet &ps, const DevTables *dev, hipStream_t stream, int num_cus, int shape,
                                  int grid_mult = 0);
-// inv_f32: the plan is admitted to the fp32 inverse (api.hip, tools/inv_bound.py); otherwise the paired fp64 one
 hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int adaptive, bool inv_f32,
                             unsigned long long *fallbacks, hipStream_t stream, int num_cus);
-// diagnostic: roundtrip8's data movement without arithmetic (roundtrip.hip)
+// diagnostic: roundtrip8_f32's data movement without arithmetic (fdct8_diag.hip)
 hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream, int num_cus);
 size_t encode_workspace_bytes(long long nbatch);
 hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *offsets,
@@ -167,6 +180,7 @@ hipError_t launch_huffman_from_pixels(const EncodeSet &es, const DevTables *dev,
                                       hipStream_t stream, int num_cus);
 hipError_t launch_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblk, int16_t *coef,
                              hipStream_t stream, int num_cus);
+// diagnostic library (fdct8_diag.hip): the lane-per-block fp64 kernels (variant 1)
 hipError_t launch_fdct8_float(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);
 hipError_t launch_idct8(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
                         long long nblk, float *recon, hipStream_t stream);

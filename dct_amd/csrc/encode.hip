@@ -20,10 +20,6 @@
 #include "fdct8_core.h"
 #include "scan_core.h"
 
-#ifndef DCTQ_ENC_GRID_MULT
-#define DCTQ_ENC_GRID_MULT DCTQ_GRID_MULT  // grid multiplier of this file's streaming kernels (dctq_internal.h)
-#endif
-
 namespace dctq {
 
 __device__ __forceinline__ void fence_rows(uint2 (&nxt)[8]) {
@@ -33,12 +29,11 @@ __device__ __forceinline__ void fence_rows(uint2 (&nxt)[8]) {
 
 __device__ __forceinline__ uint32_t nz16e(uint32_t w) { return ((w & 0xFFFFu) != 0u) + ((w >> 16) != 0u); }
 
-#ifndef DCTQ_ENC_GROUP8
-#define DCTQ_ENC_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>): -0.9 %
-#endif
-#ifndef DCTQ_ENC_WIDE
-#define DCTQ_ENC_WIDE 0  // resolve_ties_compact WIDE: at this kernel's 128-VGPR bound the wide rounds spill (A/B knob)
-#endif
+// Passes of <= 8 tie entries run 8 lanes per entry (exact_grouped<8>): -0.9 %; the wide
+// rounds spill at this kernel's 128-VGPR bound.
+constexpr bool kEncGroup8 = true;
+constexpr int kEncWide = 0;
+constexpr int kEncGridMult = DCTQ_GRID_MULT;  // grid multiplier of this file's streaming kernels (dctq_internal.h)
 
 template <bool ADAPTIVE>
 __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es, const DevTables *__restrict__ dev,
@@ -71,7 +66,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, false>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)nblk, vn, mlo, mhi);
         fence_rows(nxt);  // the prefetch wait: retires the previous batch's stores too
-        resolve_ties_compact<ADAPTIVE, DCTQ_ENC_GROUP8, DCTQ_ENC_WIDE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+        resolve_ties_compact<ADAPTIVE, kEncGroup8, kEncWide>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         wave_sync();
         u4v q[8];
         stage_chunks(stage, wv, lane, q);
@@ -101,7 +96,7 @@ template <typename K, typename... A>
 static hipError_t launch_enc(K kernel, uint32_t nbatch, int num_cus, hipStream_t stream, A... args) {
     const int per_cu = resident_per_cu(kernel, kThreads);
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_ENC_GRID_MULT);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * kEncGridMult);
     hipLaunchKernelGGL(kernel, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, args...);
     return hipGetLastError();
 }

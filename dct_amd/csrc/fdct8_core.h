@@ -11,6 +11,9 @@ namespace dctq {
 
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
+constexpr int kFWaves = 4;  // the streaming forward kernels' workgroup: 4 waves
+constexpr int kFThreads = 64 * kFWaves;
+constexpr int kV3GridMult = 16;  // fdct8_quant_v3's grid: 16 x its resident workgroups (fdct8.hip)
 constexpr int kPitch = 9;  // uint4 per block in the LDS stage: 128 B + 16 B pad
 constexpr float kMagic = 12582912.0f;  // 1.5 * 2^23: fma(y, w, kMagic) rounds y*w to an integer in its low bits
 
@@ -91,8 +94,6 @@ __device__ __forceinline__ double exact_div(double out, double m) {
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-constexpr int kQCap = 128;     // per-wave tie queue: < 64 between rounds + one round of <= 64
-static_assert(kQCap <= 128, "queue entries hold the stash slot in 7 bits");
 constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) conflicts for the b32 writes
 #ifndef DCTQ_STORE_AUX
 // Cache policy of the bulk coefficient stores (gfx950: 1 sc0, 2 nt, 16 sc1).
@@ -103,12 +104,6 @@ constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) con
 #endif
 #ifndef DCTQ_LOAD_NT
 #define DCTQ_LOAD_NT 1  // pixel rows are read exactly once
-#endif
-#ifndef DCTQ_PATCH_COND
-#define DCTQ_PATCH_COND 1  // drains store only coefficients whose exact value differs from the fast one
-#endif
-#ifndef DCTQ_STASH_DEDUP
-#define DCTQ_STASH_DEDUP 1  // one pixel stash per flagged block and batch (its entries share it)
 #endif
 #ifndef DCTQ_ABLATE
 #define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores, 2048 no final drain, 4096 drains compute but do not patch, 8192 in-stage passes without the fp64 evaluation

@@ -25,24 +25,12 @@
 #include "fdct8_core.h"
 #include "pair_core.h"
 
-#ifndef DCTQ_RT_GRID_MULT
-#define DCTQ_RT_GRID_MULT DCTQ_GRID_MULT  // grid multiplier of this file's streaming kernels (dctq_internal.h)
-#endif
-
 namespace dctq {
 
-#ifndef DCTQ_RT_EARLY_PREFETCH
-#define DCTQ_RT_EARLY_PREFETCH 1  // next batch's rows requested at the top of the batch (0: after inverse A)
-#endif
-#ifndef DCTQ_RT_OCC
-#define DCTQ_RT_OCC 4  // waves per SIMD (launch bound)
-#endif
-#ifndef DCTQ_RT_GROUP8
-#define DCTQ_RT_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>): -4.9 % on the bench step
-#endif
-#ifndef DCTQ_RT_WIDE
-#define DCTQ_RT_WIDE 0  // resolve_ties_compact WIDE: at this kernel's 128-VGPR bound the wide rounds spill (A/B knob)
-#endif
+// Passes of <= 8 tie entries run 8 lanes per entry (exact_grouped<8>): -4.9 % on the bench
+// step (round 3); the wide rounds spill at these kernels' 128-VGPR bound.
+constexpr bool kRtGroup8 = true;
+constexpr int kRtWide = 0;
 
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
 
@@ -171,34 +159,6 @@ __device__ __forceinline__ void inverse_block_f32(const DevTables *__restrict__ 
     }
 }
 
-// The 8 KiB recon half of the wave's stage (32 blocks at kPitchP, as store_stage
-// reads it) into registers, and those registers to HBM: store_stage in two steps,
-// so a caller can keep one half's store data live while it reads the next.
-__device__ __forceinline__ void stage_read_half(const uint4 *stage, int wv, int lane, u4p (&val)[8]) {
-    const char *base = reinterpret_cast<const char *>(stage) + wv * 32 * kPitchP;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint4 t = *reinterpret_cast<const uint4 *>(base + (4 * k + (lane >> 4)) * kPitchP + (lane & 15) * 16);
-        val[k] = u4p{t.x, t.y, t.z, t.w};
-    }
-}
-__device__ __forceinline__ void store_half(const u4p (&val)[8], int lane, char *dst, uint32_t nbytes) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nbytes, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
-}
-
-// Lane l writes its block's 256 B of recon at the stage slot (l & 31) -- the
-// blocks of the batch's first 32 lanes (HALF 0) or of its last 32 (HALF 1).
-template <int HALF>
-__device__ __forceinline__ void stage_recon_half(char *wstage, int lane, const float (&x)[64]) {
-    if ((lane >> 5) == HALF) {
-        float4 *dst = reinterpret_cast<float4 *>(wstage + (lane & 31) * kPitchP);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dst[r] = make_float4(x[4 * r], x[4 * r + 1], x[4 * r + 2], x[4 * r + 3]);
-    }
-}
-
 // The fused round trip with the fp32 inverse (non-adaptive plans admitted by
 // api.hip inverse_f32_bound, e.g. q <= 71 of the standard table).  Phases 1-2 are
 // roundtrip8's; phase 3 runs lane per block (no transposes, half the fp64 kernel's
@@ -209,7 +169,7 @@ __device__ __forceinline__ void stage_recon_half(char *wstage, int lane, const f
 // two halves' stores; the only waits are the prefetch fence after the forward and
 // one retire of the coefficient stores after the inverse, both behind a compute phase.
 template <bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8_f32(RoundTripSet rt,
+__global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8_f32(RoundTripSet rt,
                                                                        const DevTables *__restrict__ dev,
                                                                        unsigned long long *fallbacks) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
@@ -297,7 +257,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8_f32(RoundTri
 }
 
 template <bool ADAPTIVE, bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet rt, const DevTables *__restrict__ dev,
+__global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, const DevTables *__restrict__ dev,
                                                           unsigned long long *fallbacks) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
     __shared__ ExactTables tab;
@@ -323,7 +283,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        if (DCTQ_RT_EARLY_PREFETCH) prefetch_batch<false>(ps, g + step, lane, nxt);
+        prefetch_batch<false>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
@@ -334,7 +294,7 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
         retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
         const uint32_t ne =
-            resolve_ties_compact<ADAPTIVE, DCTQ_RT_GROUP8, DCTQ_RT_WIDE>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
+            resolve_ties_compact<ADAPTIVE, kRtGroup8, kRtWide>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
         wave_sync();
 
@@ -374,7 +334,6 @@ __global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip8(RoundTripSet
         retire_stores();
         wave_sync();
         store_stage(stage, wv, lane, recon, (nb < 32u ? nb : 32u) * 256u);
-        if (!DCTQ_RT_EARLY_PREFETCH) prefetch_batch<false>(ps, g + step, lane, nxt);
         // keep inverse B's inputs packed until here (converted early they are 64 more live VGPRs)
 #pragma unroll
         for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(qb[r].x), "+v"(qb[r].y), "+v"(qb[r].z), "+v"(qb[r].w));
@@ -397,99 +356,8 @@ static hipError_t launch_rt(const RoundTripSet &rt, const DevTables *dev, unsign
     static const int per_cu = resident_per_cu(roundtrip8<A, V, S>, kThreads);
     const uint32_t nbatch = rt.ps.first[rt.ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_RT_GRID_MULT);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * kRtGridMult);
     hipLaunchKernelGGL((roundtrip8<A, V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt, dev, fb);
-    return hipGetLastError();
-}
-
-// ============================================================================
-// Diagnostic: the data movement of roundtrip8_f32 (the kernel the bench's plan
-// runs) with no arithmetic -- the memory ceiling of that access pattern (bench.py
-// round_trip.movement_ceiling).  Same grid, occupancy bound, LDS footprint,
-// prefetch, stage writes, LDS read-backs and stores: per batch the pixel rows go
-// into the stage as the "coefficients" (8 x 1 KiB stores), then each lane's row
-// read-back, repeated, is its block's 256 B of "recon" (two halves of 8 x 1 KiB).
-// No wait is placed where the product waits behind a compute phase: a vmcnt(0)
-// with no arithmetic in front of it stalls on the memory the product overlaps
-// (round 4's version waited on its own prefetch at once and ran 6.5 % SLOWER than
-// the product: VERDICT r04).  The only waits are the ones the compiler inserts for
-// the prefetched rows before their use.  Without the retires, a read-back may land
-// in registers an older store still reads (the store-data hazard of DESIGN.md 3.1):
-// that can change the bytes this diagnostic writes, never where it writes them
-// (the buffer offsets stay live, and num_records clips every store).
-__global__ __launch_bounds__(kThreads, DCTQ_RT_OCC) void roundtrip_movement(RoundTripSet rt) {
-    __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ ExactTables tabpad;          // same LDS footprint as roundtrip8_f32
-    __shared__ uint16_t scrpad[kWaves * 64];
-    const PlaneSet &ps = rt.ps;
-    if (ps.n < 0) {  // keep the padding allocated
-        scrpad[threadIdx.x] = 0;
-        reinterpret_cast<volatile uint32_t *>(&tabpad)[threadIdx.x] = 0;
-    }
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t step = gridDim.x * kWaves;
-    uint32_t g = blockIdx.x * kWaves + wv;
-    uint2 nxt[8];
-    prefetch_batch(ps, g, lane, nxt);
-    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
-                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-    char *wstage = reinterpret_cast<char *>(stage) + wv * 64 * kPitch2;
-    for (; g < nbatch; g += step) {
-        const int k = plane_of(ps, g);
-        const uint32_t b = g - first_of(ps, k);
-        uint2 cur[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-        prefetch_batch<false>(ps, g + step, lane, nxt);
-        const BatchOut out = batch_out(ps, k, b);
-        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
-        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
-        uint2 *mine2 = reinterpret_cast<uint2 *>(wstage + lane * kPitch2);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            mine2[2 * r] = cur[r];
-            mine2[2 * r + 1] = make_uint2(cur[r].y, cur[r].x);
-        }
-        wave_sync();
-        const uint32_t nb = out.nb;
-        u4v val[8];
-        stage_chunks(stage, wv, lane, val);
-        uint2 qw[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) qw[r] = mine2[r];
-        {
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
-#pragma unroll
-            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
-        }
-        float x[64];
-#pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            x[2 * r] = __uint_as_float(qw[r & 15].x);
-            x[2 * r + 1] = __uint_as_float(qw[r & 15].y);
-        }
-        stage_recon_half<0>(wstage, lane, x);
-        wave_sync();
-        u4p va[8], vb[8];
-        stage_read_half(stage, wv, lane, va);
-        store_half(va, lane, recon, (nb < 32u ? nb : 32u) * 256u);
-        stage_recon_half<1>(wstage, lane, x);
-        wave_sync();
-        stage_read_half(stage, wv, lane, vb);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) asm volatile("" : "+v"(vb[c]) : "v"(va[c]));
-        store_half(vb, lane, recon + 32 * 256, (nb > 32u ? nb - 32u : 0u) * 256u);
-    }
-}
-
-hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream, int num_cus) {
-    static const int per_cu = resident_per_cu(roundtrip_movement, kThreads);
-    const uint32_t nbatch = rt.ps.first[rt.ps.n];
-    const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_RT_GRID_MULT);  // the same grid as launch_rt
-    hipLaunchKernelGGL(roundtrip_movement, dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt);
     return hipGetLastError();
 }
 
@@ -499,7 +367,7 @@ static hipError_t launch_rt_f32(const RoundTripSet &rt, const DevTables *dev, un
     static const int per_cu = resident_per_cu(roundtrip8_f32<V, S>, kThreads);
     const uint32_t nbatch = rt.ps.first[rt.ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
-    const uint32_t cap = (uint32_t)(num_cus * per_cu * DCTQ_RT_GRID_MULT);
+    const uint32_t cap = (uint32_t)(num_cus * per_cu * kRtGridMult);
     hipLaunchKernelGGL((roundtrip8_f32<V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt, dev, fb);
     return hipGetLastError();
 }

@@ -36,24 +36,17 @@ extern "C" {
 /* Opaque per-configuration state: the host-computed tables (D of src/dct.c:17-30,
  * Q of src/quantization.c:51-99, fast-path scale and guard tables) uploaded to
  * the device that was current at creation.  A plan is read-only after
- * creation: one plan may serve several streams at once (the only mutable
- * device state, the forward's tie stash, is kept per stream). */
+ * creation: one plan may serve several streams and threads at once, and the
+ * library keeps no per-stream device state.  Threading: the batched calls do not
+ * serialise -- after a thread's first call of an entry point on a stream (which
+ * shields the host's rand() stream from the HIP runtime, as every plan and
+ * memory call does) they take no lock and touch no global state. */
 typedef struct dctq_plan dctq_plan;
 
 /* quality is clamped to 1..100 exactly as quant_init does (src/quantization.c:26-31).
  * A plan holds only its ~4 KB of tables in device memory; it is reusable and
- * cheap to keep (one per quality is fine).  Since round 4 the product forward
- * resolves every plan's ties in place and allocates no stash; the stash below
- * serves the tie-queue kernel (v2), which only the diagnostic library still
- * launches.  The stash is the library's, one per (device, stream): allocated by
- * the first v2 launch on a stream over more 64-block batches than the device has
- * resident waves, sized to that launch's grid (8 KiB per wave,
- * at most 256 MiB on a 256-CU MI355X) and kept for later launches on the same
- * stream until dctq_stream_release.  The NULL stream and hipStreamPerThread
- * get one stash per calling thread (each thread's real stream differs).  A
- * launch captured into a hipGraph gets a stash of its own, never shared and
- * never reallocated, so replays may run at any time on any stream; it lives
- * until dctq_stream_release of the capture stream. */
+ * cheap to keep (one per quality is fine).  The forward resolves every plan's
+ * rounding ties in place and allocates nothing per launch. */
 int dctq_plan_create(int quality, int adaptive, dctq_plan **plan);
 /* Bind an existing reference-style context (block_size must be 8); its
  * quant_matrix VALUES are used, so a caller-modified table is honoured. */
@@ -165,11 +158,9 @@ int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, vo
 int dctq_huffman_bits_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *bits,
                              void *stream);
 
-/* Waits for `stream` and frees the tie-path stashes the calling thread's
- * forward launches on it hold (the direct one and every captured launch's):
- * call it before destroying a stream that ran tie-heavy forwards, and only
- * after the last replay of any graph captured on it.  A later launch on the
- * stream allocates a new stash.  No-op for a stream that holds none. */
+/* No-op, kept for ABI compatibility: until round 4 it freed the per-stream
+ * tie-path stash of the forward's queue kernel, which the product no longer
+ * launches (it lives on in the diagnostic build only).  Returns DCTQ_OK. */
 int dctq_stream_release(void *stream);
 
 /* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented

@@ -88,10 +88,10 @@ def test_fastdiv(lib):
 
 
 def test_forward_kernel_dispatch(lib):
-    """The product forward dispatch (fdct8.hip forward_kernel_for): in-place ties (v3) for
-    every plan at every size.  Since round 4 that includes tie-heavy plans (q >= 97: DC
-    divisor 1, the rational coefficients tie in ~1 block of 8), which ran on the queue
-    kernel (v2) before (profiles/r04/v3_tieheavy_ab.log)."""
+    """The product forward (fdct8.hip): in-place ties (v3) for every plan at every size.
+    Since round 4 that includes tie-heavy plans (q >= 97: DC divisor 1, the rational
+    coefficients tie in ~1 block of 8), which ran on the queue kernel (v2) before
+    (profiles/r04/v3_tieheavy_ab.log); since round 5 v2 is not in the product at all."""
     import dct_amd
     big, small = 194400, 4096  # the bench step's batches; 16 waves per CU x 256 CUs
     for q in (1, 10, 50, 90, 95, 96):
@@ -102,6 +102,45 @@ def test_forward_kernel_dispatch(lib):
         assert dct_amd.forward_kernel(q, 0, big, 256).startswith("fdct8_quant_v3"), q
         assert dct_amd.forward_kernel(q, 0, small, 256).startswith("fdct8_quant_v3"), q
     assert dct_amd.forward_kernel(50, 1, big, 256) == "fdct8_quant_v3<true, false, false>"
+
+
+def _device_kernels(path, tmp):
+    """Kernel symbols of every gfx950 code object embedded in a library
+    (llvm-objdump --offloading extracts them, llvm-readelf lists their symbols)."""
+    import glob
+    import shutil
+    llvm = "/opt/rocm/lib/llvm/bin"
+    os.makedirs(tmp, exist_ok=True)
+    local = os.path.join(tmp, os.path.basename(path))
+    shutil.copy(path, local)
+    r = subprocess.run([os.path.join(llvm, "llvm-objdump"), "--offloading", local], cwd=tmp, capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    names = set()
+    objs = glob.glob(local + ".*gfx950")
+    assert objs, os.listdir(tmp)
+    for obj in objs:
+        out = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--symbols", obj], capture_output=True,
+                             text=True).stdout
+        names |= {w for w in out.split() if w.startswith("_Z") and "." not in w}
+    return names
+
+
+def test_product_code_object_has_only_product_kernels(lib, tmp_path):
+    """the retired forward kernels (v1, the v2 tie queue), the
+    lane-per-block fp64 variants and the no-arithmetic movement twins are built into
+    libdct_amd_diag.so only (csrc/fdct8_diag.hip); the product's code objects hold the
+    kernels the product dispatch runs."""
+    prod = _device_kernels(os.path.join(ROOT, "dct_amd", "libdct_amd.so"), str(tmp_path / "p"))
+    diag = _device_kernels(os.path.join(ROOT, "dct_amd", "libdct_amd_diag.so"), str(tmp_path / "d"))
+    retired = ("fdct8_quant_v1", "fdct8_quant_v2", "fdct8_movement", "roundtrip_movement", "fdct8_float_kernel",
+               "idct8_kernel")
+    assert not [k for k in prod if any(r in k for r in retired)], sorted(prod)
+    for want in ("fdct8_quant_v3", "roundtrip8_f32", "roundtrip8I", "idct8_pair", "fdct8_float_pair",
+                 "encode_count_kernel", "huffman_bits_kernel", "synth_kernel"):
+        assert any(want in k for k in prod), (want, sorted(prod))
+    for r in retired:
+        assert any(r in k for k in diag), (r, sorted(diag))
 
 
 def test_error_strings(lib):
