@@ -695,7 +695,7 @@ def round_trip_leg(args, plan, luma, chroma, world, rank, dev):
     bpb = 64 + 128 + 256
     inv_bound, inv_f32 = dct_amd.inverse_bound(args.quality, args.adaptive)
     return {"op": "round_trip_planes (fused forward+inverse, one launch per step; BASELINE configs[4])",
-            "kernel": "roundtrip8_f32" if inv_f32 else "roundtrip8",
+            "kernel": "roundtrip8<..., INV32=true> (paired-lane fp32 inverse)" if inv_f32 else "roundtrip8 (paired-lane fp64 inverse)",
             "inverse": {"arithmetic": "fp32" if inv_f32 else "fp64",
                         "error_bound": inv_bound if inv_f32 else None,
                         "rule": "fp32 when the rigorous bound of tools/inv_bound.py for this plan is <= 5e-5 "

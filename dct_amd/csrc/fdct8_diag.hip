@@ -1,7 +1,7 @@
 // dct_amd/csrc/fdct8_diag.hip -- kernels and machinery of the DIAGNOSTIC library
 // only (libdct_amd_diag.so; dct_amd/build.py DIAG_SOURCES).  libdct_amd.so, the
 // product, carries none of it: its forward is fdct8_quant_v3 for every plan
-// (fdct8.hip), its round trip roundtrip8 / roundtrip8_f32 (roundtrip.hip).
+// (fdct8.hip), its round trip roundtrip8 (roundtrip.hip).
 //   * fdct8_quant_v1 (one workgroup per 256 blocks, divergent exact path) and
 //     fdct8_quant_v2 (the round-1/2 tie-queue kernel with its per-stream pixel
 //     stash), selected per plan by dctq_diag_plan_set_variant (1 / 4) for the
@@ -757,38 +757,21 @@ hipError_t launch_idct8(const DevTables *dev, int adaptive, const int16_t *coef,
 
 
 // ============================================================================
-// Diagnostic: the data movement of roundtrip8_f32 (the kernel the bench's plan
-// runs) with no arithmetic -- the memory ceiling of that access pattern (bench.py
+// Diagnostic: roundtrip8's data movement with no arithmetic (bench.py
 // round_trip.movement_ceiling).  Same grid, occupancy bound, LDS footprint,
-// prefetch, stage writes, LDS read-backs and stores: per batch the pixel rows go
-// into the stage as the "coefficients" (8 x 1 KiB stores), then each lane's row
-// read-back, repeated, is its block's 256 B of "recon" (two halves of 8 x 1 KiB).
-// No wait is placed where the product waits behind a compute phase: a vmcnt(0)
-// with no arithmetic in front of it stalls on the memory the product overlaps
-// (round 4's version waited on its own prefetch at once and ran 6.5 % SLOWER than
-// the product: VERDICT r04).  The only waits are the ones the compiler inserts for
-// the prefetched rows before their use.  Without the retires, a read-back may land
-// in registers an older store still reads (the store-data hazard of DESIGN.md 3.1):
-// that can change the bytes this diagnostic writes, never where it writes them
-// (the buffer offsets stay live, and num_records clips every store).
-#ifndef DCTQ_RTMV_DATA
-#define DCTQ_RTMV_DATA 0  // A/B: 1 = product-like bytes (small int16 "coefficients", recon floats in [128, 256))
-#endif
-#ifndef DCTQ_RTMV_WAIT
-#define DCTQ_RTMV_WAIT 0  // A/B: 1 = the product's vmcnt(0) points, each behind s_sleep(DCTQ_RTMV_SLEEP)
-#endif
-#ifndef DCTQ_RTMV_SLEEP
-#define DCTQ_RTMV_SLEEP 0
-#endif
-__device__ __forceinline__ void rtmv_compute_phase() {
-    if (DCTQ_RTMV_WAIT) {
-        if (DCTQ_RTMV_SLEEP) __builtin_amdgcn_s_sleep(DCTQ_RTMV_SLEEP);
-        retire_stores();
-    }
-}
+// prefetch, stage writes, LDS read-backs, stores and vmcnt(0) points as
+// roundtrip8 (the product's fp32 and fp64 instantiations share them): per batch
+// the pixel rows go into the stage as the "coefficients" (8 x 1 KiB stores), then
+// twice 32 blocks of 256 B "recon" (the rows repeated) through the paired-inverse
+// stage layout (8 x 1 KiB each), each half written to the stage, retired, stored.
+// Round 5 (profiles/r05/rt_ab.log): this twin, one without any wait, ones
+// with s_sleep where the arithmetic sits and ones writing product-like bytes all
+// run 1.5-2 % SLOWER than the product on the same box -- the product's stores
+// leave spaced by its compute phases, which this write-heavy mix takes better --
+// so it is reported beside the flat 1:2:4 stream, not as a ceiling.
 __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip_movement(RoundTripSet rt) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ ExactTables tabpad;          // same LDS footprint as roundtrip8_f32
+    __shared__ ExactTables tabpad;          // same LDS footprint as roundtrip8
     __shared__ uint16_t scrpad[kWaves * 64];
     const PlaneSet &ps = rt.ps;
     if (ps.n < 0) {  // keep the padding allocated
@@ -796,6 +779,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip_movement(RoundTrip
         reinterpret_cast<volatile uint32_t *>(&tabpad)[threadIdx.x] = 0;
     }
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5, j = lane & 31;
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kWaves;
     uint32_t g = blockIdx.x * kWaves + wv;
@@ -815,45 +799,34 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip_movement(RoundTrip
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
         uint2 *mine2 = reinterpret_cast<uint2 *>(wstage + lane * kPitch2);
-        const uint32_t cm = DCTQ_RTMV_DATA ? 0x000F000Fu : 0xFFFFFFFFu;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-            mine2[2 * r] = make_uint2(cur[r].x & cm, cur[r].y & cm);
-            mine2[2 * r + 1] = make_uint2(cur[r].y & cm, cur[r].x & cm);
+            mine2[2 * r] = cur[r];
+            mine2[2 * r + 1] = make_uint2(cur[r].y, cur[r].x);
         }
-        rtmv_compute_phase();  // the product: its forward, then the prefetch fence
+        retire_stores();  // roundtrip8: after its forward, before the tie pass's LDS reads
         wave_sync();
         const uint32_t nb = out.nb;
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
-        uint2 qw[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) qw[r] = mine2[r];
         {
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
 #pragma unroll
             for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
         }
-        float x[64];
-        const uint32_t rm = DCTQ_RTMV_DATA ? 0x007FFFFFu : 0xFFFFFFFFu, ro = DCTQ_RTMV_DATA ? 0x43000000u : 0u;
+        char *mine = wstage + j * kPitchP + h * 128;
 #pragma unroll
-        for (int r = 0; r < 32; ++r) {
-            x[2 * r] = __uint_as_float((qw[r & 15].x * 0x9E3779B1u & rm) | ro);
-            x[2 * r + 1] = __uint_as_float((qw[r & 15].y * 0x85EBCA77u & rm) | ro);
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+                *reinterpret_cast<uint4 *>(mine + r * 16) =
+                    make_uint4(cur[r].x, cur[r].y, cur[r].x ^ (uint32_t)half, cur[r].y ^ (uint32_t)lane);
+            retire_stores();  // roundtrip8: after each inverse half, before its read-back
+            wave_sync();
+            const uint32_t n32 = half ? (nb > 32u ? nb - 32u : 0u) : (nb < 32u ? nb : 32u);
+            store_stage(stage, wv, lane, recon + half * 32 * 256, n32 * 256u);
         }
-        stage_recon_half<0>(wstage, lane, x);
-        rtmv_compute_phase();  // the product: its inverse, then the retire of the coefficient stores
-        wave_sync();
-        u4p va[8], vb[8];
-        stage_read_half(stage, wv, lane, va);
-        store_half(va, lane, recon, (nb < 32u ? nb : 32u) * 256u);
-        stage_recon_half<1>(wstage, lane, x);
-        wave_sync();
-        stage_read_half(stage, wv, lane, vb);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) asm volatile("" : "+v"(vb[c]) : "v"(va[c]));
-        store_half(vb, lane, recon + 32 * 256, (nb > 32u ? nb - 32u : 0u) * 256u);
     }
 }
 

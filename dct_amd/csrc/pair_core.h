@@ -68,7 +68,14 @@ __device__ __forceinline__ void half_wave_scale(double (&v)[8], ConstDouble *lo,
 }
 
 // Stage chunk k of the wave's 8 KiB (blocks 4k..4k+3, 16 B per lane) -> HBM.
+// dst and nbytes are wave-uniform; readfirstlane says so to the compiler, which
+// otherwise may keep them in VGPRs under SGPR pressure and wrap every store in a
+// waterfall loop (the fused round trip's second half did).
 __device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane, char *dst, uint32_t nbytes) {
+    const uint64_t d = reinterpret_cast<uint64_t>(dst);
+    dst = reinterpret_cast<char *>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d >> 32)) << 32) |
+                                   __builtin_amdgcn_readfirstlane((uint32_t)d));
+    nbytes = __builtin_amdgcn_readfirstlane(nbytes);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nbytes, 0x00020000);
     const char *base = reinterpret_cast<const char *>(stage) + wv * 32 * kPitchP;
     u4p val[8];
@@ -80,34 +87,6 @@ __device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
-}
-
-// The 8 KiB recon half of the wave's stage (32 blocks at kPitchP, as store_stage
-// reads it) into registers, and those registers to HBM: store_stage in two steps,
-// so a caller can keep one half's store data live while it reads the next.
-__device__ __forceinline__ void stage_read_half(const uint4 *stage, int wv, int lane, u4p (&val)[8]) {
-    const char *base = reinterpret_cast<const char *>(stage) + wv * 32 * kPitchP;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint4 t = *reinterpret_cast<const uint4 *>(base + (4 * k + (lane >> 4)) * kPitchP + (lane & 15) * 16);
-        val[k] = u4p{t.x, t.y, t.z, t.w};
-    }
-}
-__device__ __forceinline__ void store_half(const u4p (&val)[8], int lane, char *dst, uint32_t nbytes) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nbytes, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
-}
-
-// Lane l writes its block's 256 B of recon at the stage slot (l & 31) -- the
-// blocks of the batch's first 32 lanes (HALF 0) or of its last 32 (HALF 1).
-template <int HALF>
-__device__ __forceinline__ void stage_recon_half(char *wstage, int lane, const float (&x)[64]) {
-    if ((lane >> 5) == HALF) {
-        float4 *dst = reinterpret_cast<float4 *>(wstage + (lane & 31) * kPitchP);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dst[r] = make_float4(x[4 * r], x[4 * r + 1], x[4 * r + 2], x[4 * r + 3]);
-    }
 }
 
 }  // namespace dctq

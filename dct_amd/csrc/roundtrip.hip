@@ -17,8 +17,9 @@
 //  2. the stage is read back for the 1 KiB coefficient stores AND, per lane, the
 //     two half blocks the paired inverse needs (lane (h, j): rows 4h..4h+3 of
 //     blocks j and 32 + j); var_num follows by one v_permlane32_swap;
-//  3. two paired-lane fp64 inverses (pair_core.h, as idct8_pair), 32 blocks
-//     each, staged as fp32 rows and written as 1 KiB stores.
+//  3. two paired-lane inverses (pair_core.h, as idct8_pair), 32 blocks each,
+//     staged as fp32 rows and written as 1 KiB stores: fp32 arithmetic for the
+//     plans a rigorous error bound admits (inverse_half_f32), fp64 otherwise.
 // Store-data hazard: every LDS read-back that lands in VGPRs comes
 // after a wait that retires the wave's pending stores -- the prefetch fence for
 // phase 2, an explicit vmcnt(0) before each recon read-back.
@@ -32,11 +33,16 @@ namespace dctq {
 constexpr bool kRtGroup8 = true;
 constexpr int kRtWide = 0;
 
+#ifndef DCTQ_RT_LATE_PF
+#define DCTQ_RT_LATE_PF 1
+#endif
+
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
 
-// Dequantize + inverse DCT + 128 of one 32-block sub-batch, lane (h, j) holding
-// rows 4h..4h+3 of block j (8 int16 per uint4) and the block's var_num; fp32
-// rows into the wave's stage (layout of idct8_pair).
+// Dequantize + inverse DCT + 128 of one 32-block sub-batch in fp64, lane (h, j)
+// holding rows 4h..4h+3 of block j (8 int16 per uint4) and the block's var_num;
+// fp32 rows into the wave's stage (layout of idct8_pair).  Adaptive plans and the
+// non-adaptive plans the fp32 bound does not admit.
 template <bool ADAPTIVE>
 __device__ __forceinline__ void inverse_half(const DevTables *__restrict__ dev, const uint4 (&q)[4], int32_t vn,
                                              int h, char *mine) {
@@ -120,143 +126,88 @@ __device__ __forceinline__ void aan8t_f(float &v0, float &v1, float &v2, float &
     v7 = ga0 - gb0;
 }
 
-// Dequantize + inverse DCT + 128 of the lane's own block in fp32, for the plans
-// api.hip admits (inverse_f32_bound: |recon - reference| <= 5e-5 for every input
-// block; non-adaptive only, whose dequantisation is the reference's q * (1/Q),
-// src/quantization.c:139,144): x_uv = fl32(q_uv * fl32(iscale_uv)) (one v_pk_mul per
-// coefficient pair, the scale pair in SGPRs), the columns then the rows through
-// aan8t_f (src/dct.c:80-105 as D^T X D), then + 128 (tools/inv_bound.py models
-// exactly this sequence).  qw = the block's 64 int16 (row-major, two per dword).
-__device__ __forceinline__ void inverse_block_f32(const DevTables *__restrict__ dev, const uint2 (&qw)[16],
-                                                  float (&x)[64]) {
+// The fp32 inverse (non-adaptive plans admitted by api.hip inverse_f32_bound:
+// |recon - reference| <= 5e-5 for every input block, e.g. q <= 71 of the standard
+// table; their dequantisation is the reference's q * (1/Q), src/quantization.c:139,
+// 144), in inverse_half's paired-lane layout (lane (h, j): rows 4h..4h+3 of block j):
+// x_uv = fl32(q_uv * fl32(iscale_uv)) (one v_pk_mul per coefficient pair, the scale
+// pair of the lane's half-wave in SGPRs), the columns (after the exact lane-half
+// transpose) then the rows through aan8t_f (src/dct.c:80-105 as D^T X D), then
+// + 128 -- exactly the sequence tools/inv_bound.py bounds.  Half the fp64 kernel's
+// VALU issue (profiles/r05/pmc_rt_*).  Lane per block (every lane inverting its own
+// block in registers, no transposes, the 16 KiB of recon then leaving as two 8 KiB
+// halves back to back) issued less still but ran 4.4-4.6 % slower on the bench step
+// (profiles/r05/rt_ab.log): the paired layout's stores leave in three spaced
+// groups (coefficients, half A after inverse A, half B after inverse B), which this
+// write-heavy stream (64 B read : 384 B written per block) takes better than bursts.
+__device__ __forceinline__ void swap_halves_f(float &x, float &y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]);
+    y = __uint_as_float(r[1]);
+}
+// v[k] (a row's pairs of coefficients) *= lo[k] in lanes 0-31 and *= hi[k] in lanes
+// 32-63, both scale rows in SGPR pairs: two exec-masked v_pk_mul_f32 per pair (a
+// per-lane select of the factor costs 2 v_mov + 1 v_cndmask per value).  The wave
+// is fully active here; exec is saved and restored inside the block.
+typedef const __attribute__((address_space(4))) uint64_t ConstPair;
+__device__ __forceinline__ void half_wave_scale_f32(f2 (&v)[4], ConstPair *lo, ConstPair *hi) {
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %[sv], exec\n\t"
+        "s_mov_b32 exec_hi, 0\n\t"
+        "v_pk_mul_f32 %0, %0, %5\n\tv_pk_mul_f32 %1, %1, %6\n\tv_pk_mul_f32 %2, %2, %7\n\tv_pk_mul_f32 %3, %3, %8\n\t"
+        "s_mov_b64 exec, %[sv]\n\t"
+        "s_mov_b32 exec_lo, 0\n\t"
+        "v_pk_mul_f32 %0, %0, %9\n\tv_pk_mul_f32 %1, %1, %10\n\tv_pk_mul_f32 %2, %2, %11\n\tv_pk_mul_f32 %3, %3, %12\n\t"
+        "s_mov_b64 exec, %[sv]"
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), [sv] "=&s"(save)
+        : "s"(lo[0]), "s"(lo[1]), "s"(lo[2]), "s"(lo[3]), "s"(hi[0]), "s"(hi[1]), "s"(hi[2]), "s"(hi[3]));
+}
+
+__device__ __forceinline__ void inverse_half_f32(const DevTables *__restrict__ dev, const uint4 (&q)[4], int h,
+                                                 char *mine) {
+    float v[4][8];
     ConstTables *tp = tables(dev);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const uint32_t w[2] = {qw[r].x, qw[r].y};
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t w[4] = {q[r].x, q[r].y, q[r].z, q[r].w};
+        f2 x[4];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int c = 4 * r + 2 * h;
-            const f2 q = {(float)(int)(int16_t)(w[h] & 0xFFFFu), (float)((int)w[h] >> 16)};
-            const f2 sc = {tp->iscale32[c], tp->iscale32[c + 1]};
-            const f2 v = q * sc;
-            x[c] = v.x;
-            x[c + 1] = v.y;
+        for (int k = 0; k < 4; ++k) x[k] = f2{(float)(int)(int16_t)(w[k] & 0xFFFFu), (float)((int)w[k] >> 16)};
+        // row r of the half-wave: row r (lanes 0-31) or r + 4 (lanes 32-63) of the block
+        half_wave_scale_f32(x, reinterpret_cast<ConstPair *>(&tp->iscale32[8 * r]),
+                            reinterpret_cast<ConstPair *>(&tp->iscale32[8 * (r + 4)]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[r][2 * k] = x[k].x;
+            v[r][2 * k + 1] = x[k].y;
         }
     }
 #pragma unroll
-    for (int v = 0; v < 8; ++v)
-        aan8t_f(x[v], x[8 + v], x[16 + v], x[24 + v], x[32 + v], x[40 + v], x[48 + v], x[56 + v]);
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-        aan8t_f(x[8 * i], x[8 * i + 1], x[8 * i + 2], x[8 * i + 3], x[8 * i + 4], x[8 * i + 5], x[8 * i + 6],
-                x[8 * i + 7]);
+        for (int k = 0; k < 4; ++k) swap_halves_f(v[r][k], v[r][k + 4]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        aan8t_f(v[0][k], v[1][k], v[2][k], v[3][k], v[0][k + 4], v[1][k + 4], v[2][k + 4], v[3][k + 4]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) swap_halves_f(v[r][k], v[r][k + 4]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) aan8t_f(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7]);
     const f2 k128 = {128.0f, 128.0f};
 #pragma unroll
-    for (int c = 0; c < 64; c += 2) {
-        const f2 v = f2{x[c], x[c + 1]} + k128;
-        x[c] = v.x;
-        x[c + 1] = v.y;
+    for (int r = 0; r < 4; ++r) {
+        f2 o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = f2{v[r][2 * k], v[r][2 * k + 1]} + k128;
+        *reinterpret_cast<float4 *>(mine + r * 32) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+        *reinterpret_cast<float4 *>(mine + r * 32 + 16) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
     }
 }
 
-// The fused round trip with the fp32 inverse (non-adaptive plans admitted by
-// api.hip inverse_f32_bound, e.g. q <= 71 of the standard table).  Phases 1-2 are
-// roundtrip8's; phase 3 runs lane per block (no transposes, half the fp64 kernel's
-// VALU issue: PMC profiles/r05/): every lane inverts its own block in registers,
-// then the recon leaves through the stage in two 8 KiB halves (blocks 0-31, then
-// 32-63).  The second half's read-back lands in registers disjoint from the first
-// half's pending store data (kept live across it), so no vmcnt(0) sits between the
-// two halves' stores; the only waits are the prefetch fence after the forward and
-// one retire of the coefficient stores after the inverse, both behind a compute phase.
-template <bool VAR, bool STATS>
-__global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8_f32(RoundTripSet rt,
-                                                                       const DevTables *__restrict__ dev,
-                                                                       unsigned long long *fallbacks) {
-    __shared__ uint4 stage[kThreads * kPitch2 / 16];
-    __shared__ ExactTables tab;
-    __shared__ uint16_t scr[kWaves * 64];  // resolve_ties_compact's entries
-    load_exact_tables(&tab, dev);
-    const PlaneSet &ps = rt.ps;
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nbatch = ps.first[ps.n];
-    const uint32_t step = gridDim.x * kWaves;
-    uint32_t g = blockIdx.x * kWaves + wv;
-    uint2 nxt[8];
-    prefetch_batch(ps, g, lane, nxt);
-    asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
-                 "+v"(nxt[6]), "+v"(nxt[7])::"memory");
-    uint32_t exact_count = 0;
-    char *wstage = reinterpret_cast<char *>(stage) + wv * 64 * kPitch2;
-    for (; g < nbatch; g += step) {
-        const int k = plane_of(ps, g);
-        const PlaneArgs &p = ps.pl[k];
-        const uint32_t b = g - first_of(ps, k);
-        uint2 cur[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-        const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        prefetch_batch<false>(ps, g + step, lane, nxt);
-        const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
-        char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
-        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
-
-        // ---- 1. forward into the stage; ties resolved in place
-        int32_t var_num;
-        uint32_t mlo, mhi;
-        forward_flags_batch<false, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
-        retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
-        const uint32_t ne = resolve_ties_compact<false, true, 0>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
-        if (STATS) exact_count += ne;
-        wave_sync();
-
-        // ---- 2. read-back: the coefficient chunks and the lane's own block
-        const uint32_t nb = out.nb;
-        u4v val[8];
-        stage_chunks(stage, wv, lane, val);
-        uint2 qw[16];
-        {
-            const uint2 *row = reinterpret_cast<const uint2 *>(wstage + lane * kPitch2);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) qw[r] = row[r];
-        }
-        {
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
-#pragma unroll
-            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
-            if (VAR) {
-                const __amdgpu_buffer_rsrc_t rv =
-                    __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(nb * 4u), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_NT_AUX);
-            }
-        }
-
-        // ---- 3. fp32 inverse, lane per block; recon out in two 8 KiB halves
-        float x[64];
-        inverse_block_f32(dev, qw, x);
-        stage_recon_half<0>(wstage, lane, x);
-        retire_stores();  // the coefficient stores have read their data (store-data hazard)
-        wave_sync();
-        u4p va[8], vb[8];
-        stage_read_half(stage, wv, lane, va);
-        store_half(va, lane, recon, (nb < 32u ? nb : 32u) * 256u);
-        stage_recon_half<1>(wstage, lane, x);
-        wave_sync();
-        stage_read_half(stage, wv, lane, vb);
-        // A's store data stays live until B's rows are in: B's LDS loads cannot land in it
-#pragma unroll
-        for (int c = 0; c < 8; ++c) asm volatile("" : "+v"(vb[c]) : "v"(va[c]));
-        store_half(vb, lane, recon + 32 * 256, (nb > 32u ? nb - 32u : 0u) * 256u);
-    }
-    if (STATS) {
-        uint32_t tot = exact_count;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
-        if (lane == 0 && tot) atomicAdd(fallbacks, (unsigned long long)tot);
-    }
-}
-
-template <bool ADAPTIVE, bool VAR, bool STATS>
+template <bool ADAPTIVE, bool VAR, bool STATS, bool INV32 = false>
 __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, const DevTables *__restrict__ dev,
                                                           unsigned long long *fallbacks) {
     __shared__ uint4 stage[kThreads * kPitch2 / 16];
@@ -283,7 +234,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        prefetch_batch<false>(ps, g + step, lane, nxt);
+        if (!DCTQ_RT_LATE_PF) prefetch_batch<false>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
@@ -292,7 +243,16 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
         int32_t var_num;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
-        retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
+        if (DCTQ_RT_LATE_PF) {
+            // the next batch's rows are requested only now: live across the forward they were
+            // spilled (two rows, each with a vmcnt(0) right behind its load); vmcnt(8) retires
+            // the previous batch's recon stores (older than these 8 loads: one in-order counter)
+            // before any LDS read, and leaves the loads in flight through the tie pass and inverse
+            prefetch_batch<false>(ps, g + step, lane, nxt);
+            __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+        } else {
+            retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
+        }
         const uint32_t ne =
             resolve_ties_compact<ADAPTIVE, kRtGroup8, kRtWide>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
@@ -330,14 +290,16 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
 
         // ---- 3. paired fp64 inverses, blocks 0-31 then 32-63 of the batch
         char *mine = wstage + j * kPitchP + h * 128;
-        inverse_half<ADAPTIVE>(dev, qa, (int32_t)vv[0], h, mine);
+        if constexpr (INV32) inverse_half_f32(dev, qa, h, mine);
+        else inverse_half<ADAPTIVE>(dev, qa, (int32_t)vv[0], h, mine);
         retire_stores();
         wave_sync();
         store_stage(stage, wv, lane, recon, (nb < 32u ? nb : 32u) * 256u);
         // keep inverse B's inputs packed until here (converted early they are 64 more live VGPRs)
 #pragma unroll
         for (int r = 0; r < 4; ++r) asm volatile("" : "+v"(qb[r].x), "+v"(qb[r].y), "+v"(qb[r].z), "+v"(qb[r].w));
-        inverse_half<ADAPTIVE>(dev, qb, (int32_t)vv[1], h, mine);
+        if constexpr (INV32) inverse_half_f32(dev, qb, h, mine);
+        else inverse_half<ADAPTIVE>(dev, qb, (int32_t)vv[1], h, mine);
         retire_stores();
         wave_sync();
         store_stage(stage, wv, lane, recon + 32 * 256, (nb > 32u ? nb - 32u : 0u) * 256u);
@@ -364,11 +326,12 @@ static hipError_t launch_rt(const RoundTripSet &rt, const DevTables *dev, unsign
 template <bool V, bool S>
 static hipError_t launch_rt_f32(const RoundTripSet &rt, const DevTables *dev, unsigned long long *fb,
                                 hipStream_t stream, int num_cus) {
-    static const int per_cu = resident_per_cu(roundtrip8_f32<V, S>, kThreads);
+    static const int per_cu = resident_per_cu(roundtrip8<false, V, S, true>, kThreads);
     const uint32_t nbatch = rt.ps.first[rt.ps.n];
     const uint32_t want = (nbatch + kWaves - 1) / kWaves;
     const uint32_t cap = (uint32_t)(num_cus * per_cu * kRtGridMult);
-    hipLaunchKernelGGL((roundtrip8_f32<V, S>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt, dev, fb);
+    hipLaunchKernelGGL((roundtrip8<false, V, S, true>), dim3(want < cap ? want : cap), dim3(kThreads), 0, stream, rt,
+                       dev, fb);
     return hipGetLastError();
 }
 

@@ -136,7 +136,7 @@ def test_product_code_object_has_only_product_kernels(lib, tmp_path):
     retired = ("fdct8_quant_v1", "fdct8_quant_v2", "fdct8_movement", "roundtrip_movement", "fdct8_float_kernel",
                "idct8_kernel")
     assert not [k for k in prod if any(r in k for r in retired)], sorted(prod)
-    for want in ("fdct8_quant_v3", "roundtrip8_f32", "roundtrip8I", "idct8_pair", "fdct8_float_pair",
+    for want in ("fdct8_quant_v3", "roundtrip8ILb0ELb0ELb0ELb1", "roundtrip8ILb1ELb0ELb0ELb0", "idct8_pair", "fdct8_float_pair",
                  "encode_count_kernel", "huffman_bits_kernel", "synth_kernel"):
         assert any(want in k for k in prod), (want, sorted(prod))
     for r in retired:
