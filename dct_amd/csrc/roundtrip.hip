@@ -33,10 +33,6 @@ namespace dctq {
 constexpr bool kRtGroup8 = true;
 constexpr int kRtWide = 0;
 
-#ifndef DCTQ_RT_LATE_PF
-#define DCTQ_RT_LATE_PF 1
-#endif
-
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
 
 // Dequantize + inverse DCT + 128 of one 32-block sub-batch in fp64, lane (h, j)
@@ -216,7 +212,6 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
     load_exact_tables(&tab, dev);
     const PlaneSet &ps = rt.ps;
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int h = lane >> 5, j = lane & 31;
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kWaves;
     uint32_t g = blockIdx.x * kWaves + wv;
@@ -234,7 +229,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        if (!DCTQ_RT_LATE_PF) prefetch_batch<false>(ps, g + step, lane, nxt);
+        prefetch_batch<false>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
@@ -243,16 +238,12 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
         int32_t var_num;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
-        if (DCTQ_RT_LATE_PF) {
-            // the next batch's rows are requested only now: live across the forward they were
-            // spilled (two rows, each with a vmcnt(0) right behind its load); vmcnt(8) retires
-            // the previous batch's recon stores (older than these 8 loads: one in-order counter)
-            // before any LDS read, and leaves the loads in flight through the tie pass and inverse
-            prefetch_batch<false>(ps, g + step, lane, nxt);
-            __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
-        } else {
-            retire_stores();  // the previous batch's recon stores (long issued) before any LDS read
-        }
+        // vmcnt(0): the previous batch's recon stores AND this batch's prefetch before any LDS
+        // read.  Not vmcnt(8) with the prefetch issued here instead (round 5): a VMEM
+        // instruction may read its address VGPRs as late as a store reads its data, and the
+        // tie pass's LDS loads then landed in the in-flight prefetch's address registers
+        // (an illegal address on the full-size test, profiles/r05/INDEX.md)
+        retire_stores();
         const uint32_t ne =
             resolve_ties_compact<ADAPTIVE, kRtGroup8, kRtWide>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
@@ -260,6 +251,12 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
 
         // ---- 2. read-back: coefficient chunks + the inverse's half blocks
         const uint32_t nb = out.nb;
+        // the inverse's lane roles from an opaque copy of the lane id: hoisted out of the
+        // loop, these indices and the LDS addresses made of them sat in VGPRs across the
+        // forward and pushed a prefetched row into scratch
+        int ol = lane;
+        asm volatile("" : "+v"(ol));
+        const int h = ol >> 5, j = ol & 31;
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
         const uint2 *st64 = reinterpret_cast<const uint2 *>(wstage);
