@@ -534,7 +534,8 @@ def encode_leg(args, plan, luma, chroma, world, dev):
     coefs = [coef_all[:nbs[0]], coef_all[nbs[0]:]]
     off = torch.empty(n + 1, dtype=torch.int32, device=dev)
     cap = 64 * n
-    sym = torch.empty(cap, dtype=torch.int32, device=dev)
+    sb = plan.symbol_bytes  # 2 when the plan bounds every |quantized coefficient| by 511 (q <= 90)
+    sym = torch.empty(cap, dtype=torch.int16 if sb == 2 else torch.int32, device=dev)
     ws = torch.empty(int(L.dctq_encode_workspace_bytes(n)) // 4 + 1, dtype=torch.int32, device=dev)
     cp = (C.c_void_p * 2)(*[c.data_ptr() for c in coefs])
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -552,7 +553,7 @@ def encode_leg(args, plan, luma, chroma, world, dev):
     total = int(off[n].item()) & 0xFFFFFFFF
     out = {"op": "encode_planes (forward + zigzag/RLE, count fused) over all planes", "steps": args.encode_steps,
            "blocks_per_s": world * n * args.encode_steps / el, "ms_per_step": el / args.encode_steps * 1e3,
-           "symbols_per_block": total / n, "stream_bytes_per_block": 4.0 * (1 + total / n),
+           "symbol_bytes": sb, "symbols_per_block": total / n, "stream_bytes_per_block": 4.0 + sb * total / n,
            "coefficient_bytes_per_block": 128}
     # the reference pipeline's per-block Huffman size (get_encoded_size after
     # build_huffman_codes, tests/test_entropy.c:329-341) of every block just encoded
@@ -588,7 +589,7 @@ def encode_leg(args, plan, luma, chroma, world, dev):
     if dist.is_initialized():
         def encode_gather():
             encode()
-            return shard.gather_symbols(off, sym)
+            return shard.gather_symbols(off, sym)  # 4 B per block + sb B per symbol on the wire
         el2 = timed(encode_gather)
         out.update({"gather_op": "encode + symbol-stream all_gather ("
                                  + ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()) + ")",

@@ -55,6 +55,8 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
         "dctq_rle_count": ([vp, ll, vp, vp, vp], i),
         "dctq_rle_emit": ([vp, ll, vp, vp, vp], i),
         "dctq_rle_decode": ([vp, vp, ll, vp, vp], i),
+        "dctq_rle_decode16": ([vp, vp, ll, vp, vp], i),
+        "dctq_plan_symbol_bytes": ([vp], i),
         "dctq_huffman_bits": ([vp, ll, vp, vp], i),
         "dctq_huffman_bits_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
         "dctq_stream_release": ([vp], i),
@@ -65,6 +67,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
             "dctq_diag_plan_set_num_cus": ([vp, i], i),
             "dctq_diag_plan_set_inverse": ([vp, i], i),
             "dctq_debug_inverse_bound": ([i, i, C.POINTER(i)], C.c_double),
+            "dctq_debug_symbol_bytes": ([i, i], i),
             "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_movement_v2_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_movement_grid_planes": ([vp, C.POINTER(_Plane), i, vp, i, vp], i),
@@ -296,11 +299,19 @@ class Plan:
                                             C.cast(rp, C.c_void_p), _stream_ptr(stream)))
         return outs, recons
 
+    @property
+    def symbol_bytes(self) -> int:
+        """Bytes per symbol of this plan's encoder output (dctq_plan_symbol_bytes): 2 when the
+        plan bounds every |quantized coefficient| by 511, else 4."""
+        return int(self._L.dctq_plan_symbol_bytes(self._h))
+
     def encode_planes(self, planes, outs=None, capacity=None, stream=None):
         """Forward + zigzag/RLE of up to 4 planes (the count fused into the forward launch).
-        Returns (coefs [int16 [nblk_k, 64]], offsets int32 [N+1], symbols int32 [total]) -- the
-        offsets/symbols hold the uint32 bit patterns, blocks numbered plane by plane; capacity
-        defaults to the worst case (64 per block).  Reads the total back (one sync)."""
+        Returns (coefs [int16 [nblk_k, 64]], offsets int32 [N+1], symbols [total]) -- offsets
+        hold uint32 bit patterns, blocks numbered plane by plane; symbols in the plan's format:
+        int32 holding (uint16)value | run << 16, or (symbol_bytes 2) int16 holding
+        run << 10 | (value & 0x3FF).  capacity (symbols) defaults to the worst case (64 per
+        block).  Reads the total back (one sync)."""
         import torch
         n = len(planes)
         descs = (_Plane * n)(*[plane_desc(px) for px in planes])
@@ -312,7 +323,7 @@ class Plan:
         _need_planes(outs, None, None, nbs, planes)
         cap = 64 * nb if capacity is None else int(capacity)
         off = torch.empty(nb + 1, dtype=torch.int32, device=dev)
-        sym = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        sym = torch.empty(max(cap, 1), dtype=torch.int16 if self.symbol_bytes == 2 else torch.int32, device=dev)
         ws = torch.empty(int(self._L.dctq_encode_workspace_bytes(nb)) // 4 + 1, dtype=torch.int32, device=dev)
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         self._chk(self._L.dctq_encode_planes(self._h, descs, n, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
@@ -406,15 +417,22 @@ def huffman_bits(coef, out=None, stream=None):
 
 
 def rle_decode(symbols, offsets, out=None, stream=None):
-    """Inverse of rle_encode: int16 [N, 64] blocks (run_length_decode + zigzag_to_block)."""
+    """Inverse of rle_encode / encode_planes: int16 [N, 64] blocks (run_length_decode +
+    zigzag_to_block).  int16 symbols are the 2-byte format (dctq_rle_decode16)."""
     import torch
     n = offsets.numel() - 1
     if out is None:
         out = torch.empty((n, 64), dtype=torch.int16, device=offsets.device)
     _need(out, n * 64, torch.int16, "out", offsets.device)
-    _check(lib().dctq_rle_decode(C.c_void_p(symbols.data_ptr()), C.c_void_p(offsets.data_ptr()), n,
-                                 C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    fn = lib().dctq_rle_decode16 if symbols.dtype == torch.int16 else lib().dctq_rle_decode
+    _check(fn(C.c_void_p(symbols.data_ptr()), C.c_void_p(offsets.data_ptr()), n, C.c_void_p(out.data_ptr()),
+              _stream_ptr(stream)))
     return out
+
+
+def symbol_bytes(quality: int, adaptive: bool = False) -> int:
+    """Host-only: the encoder's symbol format of a standard-table plan (2 or 4 bytes)."""
+    return int(diag().dctq_debug_symbol_bytes(int(quality), int(bool(adaptive))))
 
 
 def synth(seed: int, kind, width: int, height: int, nframes: int = 1, device="cuda", stream=None, out=None):

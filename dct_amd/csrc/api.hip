@@ -139,6 +139,21 @@ double dctq::inverse_f32_bound(const dctq::DevTables &t) {
     return worst;
 }
 
+int dctq::max_abs_quantized(const dctq::DevTables &t) {
+    double l1[8];
+    for (int r = 0; r < 8; ++r) {
+        l1[r] = 0.0;
+        for (int c = 0; c < 8; ++c) l1[r] += fabs(t.dct[r * 8 + c]);
+    }
+    int m = 0;
+    for (int k = 0; k < 64; ++k) {
+        const double cmax = 128.0 * l1[k >> 3] * l1[k & 7] * (1.0 + 1e-12);
+        const int q = (int)floor(cmax / t.quant[k] + 0.5 + 1e-9);
+        m = q > m ? q : m;
+    }
+    return m;
+}
+
 static int build_plan(const double *q, int quality, int adaptive, dctq_plan **out) {
     if (!out) return fail(DCTQ_EINVAL, "plan pointer is NULL");
     for (int c = 0; c < 64; ++c)
@@ -171,6 +186,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
     for (int c = 0; c < 64; ++c) p->host.iscale32[c] = (float)p->host.iscale[c];
     p->inv_bound = dctq::inverse_f32_bound(p->host);
     p->inv_f32 = !p->adaptive && p->inv_bound <= kInvTol;
+    p->symbol_bytes = dctq::max_abs_quantized(p->host) <= 511 ? 2 : 4;
     p->host.fast = p->fast;
     hipError_t e = hipMalloc(&p->dev, sizeof(dctq::DevTables));
     if (e != hipSuccess) {
@@ -393,13 +409,16 @@ size_t dctq_encode_workspace_bytes(long long total_blocks) {
     return dctq::encode_workspace_bytes((total_blocks < 1 ? 1 : total_blocks) / 64 + dctq::kMaxPlanes + 1);
 }
 
+int dctq_plan_symbol_bytes(const dctq_plan *plan) { return plan ? plan->symbol_bytes : DCTQ_EINVAL; }
+
 int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
-                       uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
+                       uint32_t *offsets, void *symbols, long long symbols_capacity, void *workspace,
                        void *stream) {
     DCTQ_LAUNCH(stream, 2);
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!offsets || !workspace) return fail(DCTQ_EINVAL, "offsets/workspace is NULL");
     if (symbols_capacity < 0) return fail(DCTQ_EINVAL, "symbols_capacity < 0");
+    if (((uintptr_t)symbols) % 4) return fail(DCTQ_EINVAL, "symbols must be 4-byte aligned");
     dctq::EncodeSet es = {};
     int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &es.ps);
     if (rc) return rc;
@@ -410,7 +429,7 @@ int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int npla
         if (blocks >= (1ll << 26)) return fail(DCTQ_EINVAL, "more than 2^26 - 1 blocks in one encode");
     }
     es.blk_first[nplanes] = (uint32_t)blocks;
-    HIPCHK(dctq::launch_encode(es, plan->dev, plan->adaptive, offsets, symbols,
+    HIPCHK(dctq::launch_encode(es, plan->dev, plan->adaptive, offsets, symbols, plan->symbol_bytes,
                                symbols ? (unsigned long long)symbols_capacity : 0ull, workspace, (hipStream_t)stream,
                                plan->num_cus),
            "encode launch");
@@ -498,7 +517,7 @@ int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offset
     DCTQ_LAUNCH(stream, 7);
     if (int rc = rle_args(coef, offsets, nblocks)) return rc;
     if (!symbols) return fail(DCTQ_EINVAL, "symbols is NULL");
-    HIPCHK(dctq::launch_rle_emit(coef, nblocks, offsets, symbols, ~0ull, (hipStream_t)stream, device_cus()),
+    HIPCHK(dctq::launch_rle_emit(coef, nblocks, offsets, symbols, 4, ~0ull, (hipStream_t)stream, device_cus()),
            "rle_emit launch");
     return DCTQ_OK;
 }
@@ -508,8 +527,19 @@ int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long 
     DCTQ_LAUNCH(stream, 8);
     if (int rc = rle_args(symbols, offsets, nblocks)) return rc;
     if (!coef) return fail(DCTQ_EINVAL, "coef is NULL");
-    HIPCHK(dctq::launch_rle_decode(symbols, offsets, nblocks, coef, (hipStream_t)stream, device_cus()),
+    HIPCHK(dctq::launch_rle_decode(symbols, 4, offsets, nblocks, coef, (hipStream_t)stream, device_cus()),
            "rle_decode launch");
+    return DCTQ_OK;
+}
+
+int dctq_rle_decode16(const uint16_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
+                      void *stream) {
+    DCTQ_LAUNCH(stream, 12);
+    if (int rc = rle_args(symbols, offsets, nblocks)) return rc;
+    if (!coef) return fail(DCTQ_EINVAL, "coef is NULL");
+    if (((uintptr_t)symbols) % 4) return fail(DCTQ_EINVAL, "symbols must be 4-byte aligned");
+    HIPCHK(dctq::launch_rle_decode(symbols, 2, offsets, nblocks, coef, (hipStream_t)stream, device_cus()),
+           "rle_decode16 launch");
     return DCTQ_OK;
 }
 

@@ -88,6 +88,8 @@ int dctq_debug_fastdiv(uint32_t d, uint32_t n);
  * standard-table plan (api.hip inverse_f32_bound); *admitted = whether
  * dctq_round_trip_planes runs that inverse for it (non-adaptive, bound <= 5e-5). */
 double dctq_debug_inverse_bound(int quality, int adaptive, int *admitted);
+/* The encoder's symbol bytes (2 or 4) for a standard-table plan (dctq_plan_symbol_bytes). */
+int dctq_debug_symbol_bytes(int quality, int adaptive);
 
 #ifdef __cplusplus
 }

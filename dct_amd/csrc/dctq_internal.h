@@ -159,8 +159,9 @@ hipError_t launch_roundtrip(const RoundTripSet &rt, const DevTables *dev, int ad
 // diagnostic: roundtrip8_f32's data movement without arithmetic (fdct8_diag.hip)
 hipError_t launch_roundtrip_movement(const RoundTripSet &rt, hipStream_t stream, int num_cus);
 size_t encode_workspace_bytes(long long nbatch);
-hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *offsets,
-                         uint32_t *symbols, unsigned long long capacity, void *ws, hipStream_t stream, int num_cus);
+// symbol_bytes 4: (uint16)value | run << 16; 2: run << 10 | (value & 0x3FF), |value| <= 511 (rle.hip)
+hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *offsets, void *symbols,
+                         int symbol_bytes, unsigned long long capacity, void *ws, hipStream_t stream, int num_cus);
 hipError_t launch_fdct8_float_pair(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream,
                                    int num_cus);
 hipError_t launch_idct8_pair(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
@@ -172,14 +173,14 @@ hipError_t launch_rle_fixup(uint32_t *offsets, long long nblk, const void *ws, l
                             uint32_t *total_out, hipStream_t stream);
 hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offsets, void *ws, hipStream_t stream,
                             int num_cus);
-hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,
-                           unsigned long long capacity, hipStream_t stream, int num_cus);
+hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, void *symbols,
+                           int symbol_bytes, unsigned long long capacity, hipStream_t stream, int num_cus);
 // per-block Huffman size estimate (huffman.hip)
 hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bits, hipStream_t stream, int num_cus);
 hipError_t launch_huffman_from_pixels(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *bits,
                                       hipStream_t stream, int num_cus);
-hipError_t launch_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblk, int16_t *coef,
-                             hipStream_t stream, int num_cus);
+hipError_t launch_rle_decode(const void *symbols, int symbol_bytes, const uint32_t *offsets, long long nblk,
+                             int16_t *coef, hipStream_t stream, int num_cus);
 // diagnostic library (fdct8_diag.hip): the lane-per-block fp64 kernels (variant 1)
 hipError_t launch_fdct8_float(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);
 hipError_t launch_idct8(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,

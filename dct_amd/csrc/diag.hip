@@ -116,6 +116,14 @@ double dctq_debug_inverse_bound(int quality, int adaptive, int *admitted) {
     return b;
 }
 
+int dctq_debug_symbol_bytes(int quality, int adaptive) {
+    (void)adaptive;  // adaptive divisors Q (2 - nv) >= Q: the same bound
+    dctq::DevTables t;
+    dctq_host::dct_matrix(8, t.dct);
+    dctq_host::quant_matrix(8, dctq_host::clamp_quality(quality), t.quant);
+    return dctq::max_abs_quantized(t) <= 511 ? 2 : 4;
+}
+
 int dctq_diag_plan_set_num_cus(dctq_plan *plan, int num_cus) {
     DCTQ_ENTRY;
     if (!plan) return dctq::fail(DCTQ_EINVAL, "plan is NULL");

@@ -103,8 +103,8 @@ static hipError_t launch_enc(K kernel, uint32_t nbatch, int num_cus, hipStream_t
 
 size_t encode_workspace_bytes(long long nbatch) { return rle_scan_workspace_bytes(nbatch); }
 
-hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *offsets,
-                         uint32_t *symbols, unsigned long long capacity, void *ws, hipStream_t stream, int num_cus) {
+hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive, uint32_t *offsets, void *symbols,
+                         int symbol_bytes, unsigned long long capacity, void *ws, hipStream_t stream, int num_cus) {
     const uint32_t nbatch = es.ps.first[es.ps.n];
     uint32_t *tiles = (uint32_t *)ws;
     hipError_t e = adaptive ? launch_enc(encode_count_kernel<true>, nbatch, num_cus, stream, es, dev, offsets, tiles)
@@ -119,8 +119,8 @@ hipError_t launch_encode(const EncodeSet &es, const DevTables *dev, int adaptive
     }
     if (!symbols || capacity == 0) return hipSuccess;  // coefficients and offsets only
     for (int k = 0; k < es.ps.n; ++k)
-        if ((e = launch_rle_emit(es.ps.coef[k], es.ps.pl[k].nblk, offsets + es.blk_first[k], symbols, capacity, stream,
-                                 num_cus)) != hipSuccess)
+        if ((e = launch_rle_emit(es.ps.coef[k], es.ps.pl[k].nblk, offsets + es.blk_first[k], symbols, symbol_bytes,
+                                 capacity, stream, num_cus)) != hipSuccess)
             return e;
     return hipSuccess;
 }

@@ -15,6 +15,7 @@ struct dctq_plan {
     unsigned long long *fallbacks;
     int inv_f32;                 // round trip: fp32 inverse admitted (|recon err| <= inv_bound <= kInvTol)
     double inv_bound;            // the fp32 inverse's rigorous error bound for this plan (idct8_bound.h)
+    int symbol_bytes;            // the encoder's symbol format: 2 when every |quantized coefficient| <= 511, else 4
 };
 
 namespace dctq {
@@ -32,6 +33,10 @@ void dc_const_table(const double *d, const double *q, int16_t *tab);
 // rigorous bound of |recon - reference| of the fused round trip's fp32 inverse for the
 // plan's tables (non-adaptive dequantisation; tools/inv_bound.py, idct8_bound.h)
 double inverse_f32_bound(const DevTables &t);
+// the largest |quantized coefficient| a plan's table admits for u8 input: |c_uv| <=
+// 128 L1(D_u) L1(D_v) (centred pixels), |q| <= round(c_max / M) with M >= Q (adaptive
+// divisors Q (2 - nv) >= Q; the DC keeps Q)
+int max_abs_quantized(const DevTables &t);
 }  // namespace dctq
 // the admission tolerance of that bound (== idct8_bound.h kInvTol; api.hip checks they agree)
 constexpr double kInvTolDiag = 5e-5;

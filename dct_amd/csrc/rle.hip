@@ -6,7 +6,13 @@
 // nonzero zigzag element, its run = zeros before it, plus always a symbol for
 // the last element (7,7), whose run also counts itself when it is zero.  So a
 // block has exactly 1 + nnz(first 63 zigzag elements) symbols.  Blocks are
-// concatenated in order; symbol = (uint16)value | run << 16.
+// concatenated in order.  Two symbol formats (round 5):
+//   W = 4 (uint32): (uint16)value | run << 16 -- any int16 value;
+//   W = 2 (uint16): run << 10 | (value & 0x3FF) -- |value| <= 511, which a plan
+//         guarantees when its Q table bounds every quantized coefficient there
+//         (api.hip symbol_bytes; q <= 90 of the standard table): 2 B per symbol,
+//         so dense noise's 45.7 symbols per block take 91 B instead of 183 B --
+//         less than the 128 B of int16 coefficients they shrink.
 //
 // Layout choices (DESIGN.md "RLE"): one WAVE per block -- lane i holds zigzag
 // element i, so "nonzero" is a ballot, a symbol's index is mbcnt of that ballot,
@@ -27,6 +33,24 @@ namespace dctq {
 #endif
 constexpr int kRleWaves = 4;
 constexpr int kRleThreads = 64 * kRleWaves;
+
+// A symbol of value v (int16 bits in the low half of `v16`) and run r in format W.
+template <int W>
+__device__ __forceinline__ uint32_t pack_sym(uint32_t v16, uint32_t r) {
+    if constexpr (W == 4) return (v16 & 0xFFFFu) | (r << 16);
+    else return (r << 10) | (v16 & 0x3FFu);
+}
+// ... and back: the run, and the value as int16 bits (sign-extended from 10 bits for W = 2)
+template <int W>
+__device__ __forceinline__ uint32_t sym_run(uint32_t s) {
+    if constexpr (W == 4) return s >> 16;
+    else return (s >> 10) & 0x3Fu;
+}
+template <int W>
+__device__ __forceinline__ int16_t sym_value(uint32_t s) {
+    if constexpr (W == 4) return (int16_t)(s & 0xFFFFu);
+    else return (int16_t)((int32_t)(s << 22) >> 22);
+}
 
 __device__ __forceinline__ uint64_t lane_mask_below(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
@@ -226,6 +250,7 @@ constexpr int kMaxChunks = 16;  // chunks of 64 symbols per flush round
 // zigzag elements in registers (~6 VALU per element, no cross-lane work) and
 // writes its symbols at offsets[b] - offsets[64t] into LDS, which then leaves
 // as coalesced dword stores.  Denser tiles take the wave-per-block path.
+template <int W>
 __device__ __forceinline__ void emit_lane_walk(const char *lt, char *ls, int lane, uint32_t base) {
     uint32_t z[32];  // block `lane`, natural order, two elements per dword
 #pragma unroll
@@ -244,18 +269,23 @@ __device__ __forceinline__ void emit_lane_walk(const char *lt, char *ls, int lan
         const int c = kZzStatic[i];
         const uint32_t w = z[c >> 1];
         const bool nz = (c & 1) ? w > 0xFFFFu : (w & 0xFFFFu) != 0u;
-        // (uint16)value | run << 16; the last element's run counts itself when zero
+        // the last element's run counts itself when zero
         const uint32_t r = (i == 63 && !nz) ? run + 1u : run;
-        const uint32_t sym = __builtin_amdgcn_perm(r, w, (c & 1) ? 0x05040302u : 0x05040100u);
-        *reinterpret_cast<uint32_t *>(ls + pos * 4u) = sym;
+        if constexpr (W == 4) {  // (uint16)value | run << 16
+            const uint32_t sym = __builtin_amdgcn_perm(r, w, (c & 1) ? 0x05040302u : 0x05040100u);
+            *reinterpret_cast<uint32_t *>(ls + pos * 4u) = sym;
+        } else {
+            *reinterpret_cast<uint16_t *>(ls + pos * 2u) = (uint16_t)pack_sym<2>((c & 1) ? w >> 16 : w, r);
+        }
         pos += nz ? 1u : 0u;
         run = nz ? 0u : run + 1u;
     }
 }
 
+template <int W>
 __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                const uint32_t *__restrict__ offsets,
-                                                               uint32_t *__restrict__ symbols, long long ntiles,
+                                                               void *__restrict__ symbols, long long ntiles,
                                                                unsigned long long capacity) {
     __shared__ u4r tiles_lds[kRleWaves][kEmitLds / 16];
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -298,12 +328,52 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
         // 32-bit voffset small (the stream itself may exceed 4 GiB); symbols at or
         // past `capacity` are dropped by num_records
         const unsigned long long room = capacity > o0 ? capacity - o0 : 0ull;
-        if (nsym <= kLaneWalkMax) {
-            if (lane < nb) emit_lane_walk(lt, lt, lane, offv - o0);
+        if (W == 2 && nsym <= kLaneWalkMax) {
+            // 2-B symbols: the tile's stream is staged one unit late when it starts at an
+            // odd unit, so LDS dword j is global dword (o0 - pad) / 2 + j; the dwords that
+            // hold one of the tile's units and one of a neighbour's (or one past
+            // `capacity`) are written as that one unit, every other dword whole
+            const uint32_t pad = o0 & 1u;
+            if (lane < nb) emit_lane_walk<2>(lt, lt, lane, offv - o0 + pad);
+            wave_sync_lds();
+            const unsigned long long first = o0 - pad;  // even: the descriptor base is 4-B aligned
+            const unsigned long long cap = capacity > first ? capacity - first : 0ull;  // units below capacity
+            const uint32_t end = (uint32_t)(cap < pad + nsym ? cap : pad + nsym);      // units [pad, end) land
+            const __amdgpu_buffer_rsrc_t rsym = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<uint16_t *>(symbols) + first, (short)0, (int)((end + 1u) & ~1u) * 2, 0x00020000);
+            const uint32_t ndw = (end + 1u) >> 1;
+#pragma unroll
+            for (int r = 0; r < (int)((kLaneWalkMax / 2 + 1 + 1023) / 1024); ++r) {
+                if (r * 1024 >= (int)ndw) break;
+                if (r) __builtin_amdgcn_s_waitcnt(0x0F70);
+                uint32_t v[kMaxChunks];
+#pragma unroll
+                for (int j = 0; j < kMaxChunks; ++j)
+                    v[j] = *reinterpret_cast<const uint32_t *>(lt + ((r * kMaxChunks + j) * 64 + lane) * 4);
+#pragma unroll
+                for (int g = 0; g < kMaxChunks; g += 4)
+                    if ((r * kMaxChunks + g) * 64 < (int)ndw) {
+#pragma unroll
+                        for (int j = g; j < g + 4; ++j) {
+                            const uint32_t d = (uint32_t)((r * kMaxChunks + j) * 64 + lane);
+                            const bool lo = 2 * d >= pad && 2 * d < end, hi = 2 * d + 1 < end;
+                            if (lo && hi)
+                                __builtin_amdgcn_raw_buffer_store_b32(v[j], rsym, d * 4u, 0, 0);
+                            else if (lo)
+                                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[j], rsym, d * 4u, 0, 0);
+                            else if (hi)
+                                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[j] >> 16), rsym, d * 4u + 2u, 0, 0);
+                        }
+                    }
+            }
+            continue;
+        }
+        if (W == 4 && nsym <= kLaneWalkMax) {
+            if (lane < nb) emit_lane_walk<4>(lt, lt, lane, offv - o0);
             wave_sync_lds();
             const uint32_t nrec = (uint32_t)(room < nsym ? room : nsym) * 4u;
-            const __amdgpu_buffer_rsrc_t rsym =
-                __builtin_amdgcn_make_buffer_rsrc(symbols + o0, (short)0, (int)nrec, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rsym = __builtin_amdgcn_make_buffer_rsrc(
+                reinterpret_cast<uint32_t *>(symbols) + o0, (short)0, (int)nrec, 0x00020000);
             // all LDS reads of a round first, then its stores (store-data hazard):
             // chunks of 64 symbols in guarded groups of 4, the tail clipped by num_records;
             // a second round (past 1 024 symbols) starts after a vmcnt(0)
@@ -332,7 +402,8 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
             z[u] = (uint32_t)*reinterpret_cast<const uint16_t *>(lt + 2 * u * kEmitPitch + zoff) |
                    ((uint32_t)*reinterpret_cast<const uint16_t *>(lt + (2 * u + 1) * kEmitPitch + zoff) << 16);
         const __amdgpu_buffer_rsrc_t rsym = __builtin_amdgcn_make_buffer_rsrc(
-            symbols + o0, (short)0, (int)((room < 4096ull ? room : 4096ull) * 4u), 0x00020000);
+            reinterpret_cast<char *>(symbols) + o0 * (unsigned long long)W, (short)0,
+            (int)((room < 4096ull ? room : 4096ull) * W), 0x00020000);
 #pragma unroll
         for (int u = 0; u < 64; ++u) {
             const uint32_t val = (u & 1) ? z[u >> 1] >> 16 : z[u >> 1] & 0xFFFFu;
@@ -350,7 +421,13 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
             // against unconditional stores aimed past num_records, tools/rle_ab.py); the
             // vmcnt(0) at the top of the next tile is explicit, so LLVM's waitcnt
             // placement around predicated stores does not matter here
-            if (emit && u < nb) __builtin_amdgcn_raw_buffer_store_b32(val | (runlen << 16), rsym, (o - o0 + idx) * 4u, 0, 0);
+            if (emit && u < nb) {
+                if constexpr (W == 4)
+                    __builtin_amdgcn_raw_buffer_store_b32(pack_sym<4>(val, runlen), rsym, (o - o0 + idx) * 4u, 0, 0);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)pack_sym<2>(val, runlen), rsym, (o - o0 + idx) * 2u, 0,
+                                                          0);
+            }
         }
     }
 }
@@ -404,7 +481,21 @@ constexpr int kDecBatch = 16;  // symbols per lane per step
 constexpr int kDecLds = kHalf * 128 + 240 * 4;  // >= kHalf * kDecPitch
 static_assert(kDecLds >= kHalf * kDecPitch, "walk path tile");
 
-__global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32_t *__restrict__ symbols,
+// 2-B symbols widened to the 4-B format in registers: the decode paths below then
+// run unchanged.  Units sit two per dword; a lane whose units start at an odd unit
+// loads from the dword before and shifts by 16 bits (v_alignbit).
+__device__ __forceinline__ uint32_t widen16(uint32_t u) {
+    return pack_sym<4>((uint32_t)(uint16_t)sym_value<2>(u), sym_run<2>(u));
+}
+// units [u, u + 2N) from dword-aligned `d` (N + 1 dwords: d[0] holds unit u & ~1)
+template <int N>
+__device__ __forceinline__ void align_units(const uint32_t (&d)[N + 1], uint32_t odd, uint32_t (&out)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = __builtin_amdgcn_alignbit(d[k + 1], d[k], odd * 16u);
+}
+
+template <int W>
+__global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const void *__restrict__ symbols,
                                                                  const uint32_t *__restrict__ offsets, long long nblk,
                                                                  int16_t *__restrict__ coef, long long ntiles) {
     __shared__ u4r wave_lds[kRleWaves][kDecLds / 16];
@@ -430,11 +521,16 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
             const bool walk = !lane_path && kDecWalkMax && nh <= kDecWalkMax;
             if (lane_path) {
                 const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
+                    const_cast<char *>(reinterpret_cast<const char *>(symbols)) + (unsigned long long)s0 * W, (short)0,
+                    (int)(nh * W), 0x00020000);
                 uint32_t v[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j)  // past nh: clipped to 0, no traffic
-                    v[j] = __builtin_amdgcn_raw_buffer_load_b32(rsy, (j * 64 + lane) * 4, 0, 0);
+                for (int j = 0; j < 4; ++j) {  // past nh: clipped to 0, no traffic
+                    if constexpr (W == 4)
+                        v[j] = __builtin_amdgcn_raw_buffer_load_b32(rsy, (j * 64 + lane) * 4, 0, 0);
+                    else
+                        v[j] = widen16(__builtin_amdgcn_raw_buffer_load_b16(rsy, (j * 64 + lane) * 2, 0, 0));
+                }
                 // block h+i's start and count, to lane i
                 const uint32_t my_off = (uint32_t)__shfl((int)offv, (lane + h) & 63);
                 const uint32_t my_cnt = (uint32_t)__shfl((int)cnt_lane, (lane + h) & 63);
@@ -459,19 +555,46 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
                     pos += 1u;
                 }
             } else if (walk) {
-                // the half's symbols; loads past them (any lane, any offsets) are clipped to 0
+                // the half's symbols; loads past them (any lane, any offsets) are clipped to 0.
+                // 2-B units: the descriptor starts at the even unit at or before s0 and ends on
+                // a whole dword (one unit past the half at most: inside the stream's 4-B-aligned
+                // allocation)
+                const uint32_t pad = W == 2 ? (s0 & 1u) : 0u;
                 const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
+                    const_cast<char *>(reinterpret_cast<const char *>(symbols)) + (unsigned long long)(s0 - pad) * W,
+                    (short)0, (int)(W == 4 ? nh * 4u : ((pad + nh + 1u) & ~1u) * 2u), 0x00020000);
                 const uint32_t my_off = (uint32_t)__shfl((int)offv, (lane + h) & 63);
                 const uint32_t my_cnt = (uint32_t)__shfl((int)cnt_lane, (lane + h) & 63);
                 const uint32_t cnt = lane < he - h ? (my_cnt < 64u ? my_cnt : 64u) : 0u;
-                const uint32_t rel = (my_off - s0) * 4u;
+                const uint32_t urel = my_off - s0 + pad;  // the block's first unit from the descriptor base
+                const uint32_t rel = W == 4 ? (my_off - s0) * 4u : (urel & ~1u) * 2u, odd = urel & 1u;
                 auto load_batch = [&](uint32_t i, u4r (&q)[kDecBatch / 4]) {
+                    if constexpr (W == 4) {
 #pragma unroll
-                    for (int k = 0; k < kDecBatch / 4; ++k)
-                        q[k] = i + 4 * k < cnt
-                                   ? __builtin_amdgcn_raw_buffer_load_b128(rsy, rel + (i + 4 * k) * 4u, 0, 0)
-                                   : u4r{0u, 0u, 0u, 0u};
+                        for (int k = 0; k < kDecBatch / 4; ++k)
+                            q[k] = i + 4 * k < cnt
+                                       ? __builtin_amdgcn_raw_buffer_load_b128(rsy, rel + (i + 4 * k) * 4u, 0, 0)
+                                       : u4r{0u, 0u, 0u, 0u};
+                    } else {  // kDecBatch units = 8 dwords, from 9 aligned ones
+                        uint32_t d[kDecBatch / 2 + 1];
+#pragma unroll
+                        for (int k = 0; k < kDecBatch / 8; ++k) {
+                            // dwords 4k..4k+3 hold units i + 8k - odd .. i + 8k - odd + 7
+                            const u4r t = i + 8 * k < cnt + odd
+                                              ? __builtin_amdgcn_raw_buffer_load_b128(rsy, rel + (i + 8 * k) * 2u, 0, 0)
+                                              : u4r{0u, 0u, 0u, 0u};
+                            d[4 * k] = t[0], d[4 * k + 1] = t[1], d[4 * k + 2] = t[2], d[4 * k + 3] = t[3];
+                        }
+                        d[kDecBatch / 2] = odd && i + kDecBatch - 1 < cnt
+                                               ? __builtin_amdgcn_raw_buffer_load_b32(rsy, rel + (i + kDecBatch) * 2u, 0, 0)
+                                               : 0u;
+                        uint32_t a[kDecBatch / 2];
+                        align_units<kDecBatch / 2>(d, odd, a);
+#pragma unroll
+                        for (int k = 0; k < kDecBatch / 4; ++k)
+                            q[k] = u4r{widen16(a[2 * k]), widen16(a[2 * k] >> 16), widen16(a[2 * k + 1]),
+                                       widen16(a[2 * k + 1] >> 16)};
+                    }
                 };
                 u4r cur[kDecBatch / 4];
                 load_batch(0, cur);
@@ -503,16 +626,30 @@ __global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const uint32
                 // Quad path: 4 blocks per step, one per 16-lane row; lane s of a row holds its
                 // block's symbols 4s..4s+3 (one 16-B load: 4 symbols per lane-address). Positions:
                 // a 4-element prefix in the lane, then a row-segmented DPP scan of the lane totals.
+                const uint32_t pad = W == 2 ? (s0 & 1u) : 0u;  // as the walk path
                 const __amdgpu_buffer_rsrc_t rsy = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint32_t *>(symbols) + s0, (short)0, (int)(nh * 4u), 0x00020000);
+                    const_cast<char *>(reinterpret_cast<const char *>(symbols)) + (unsigned long long)(s0 - pad) * W,
+                    (short)0, (int)(W == 4 ? nh * 4u : ((pad + nh + 1u) & ~1u) * 2u), 0x00020000);
                 const int r = lane >> 4, s4 = 4 * (lane & 15);
                 auto group_load = [&](int g, u4r &q, uint32_t &cnt) {
                     const int b = h + 4 * g + r;  // this row's block (past `he`: none)
                     const uint32_t ob = (uint32_t)__shfl((int)offv, b & 63);
                     const uint32_t cb = (uint32_t)__shfl((int)cnt_lane, b & 63);
                     cnt = b < he ? (cb < 64u ? cb : 64u) : 0u;
-                    q = (uint32_t)s4 < cnt ? __builtin_amdgcn_raw_buffer_load_b128(rsy, (ob - s0 + s4) * 4u, 0, 0)
-                                           : u4r{0u, 0u, 0u, 0u};
+                    if constexpr (W == 4) {
+                        q = (uint32_t)s4 < cnt ? __builtin_amdgcn_raw_buffer_load_b128(rsy, (ob - s0 + s4) * 4u, 0, 0)
+                                               : u4r{0u, 0u, 0u, 0u};
+                    } else {  // units s4..s4+3 = 2 dwords, from 3 aligned ones
+                        const uint32_t u = ob - s0 + pad + (uint32_t)s4, odd = u & 1u;
+                        uint32_t d[3] = {0u, 0u, 0u};
+                        if ((uint32_t)s4 < cnt) {
+                            const auto t = __builtin_amdgcn_raw_buffer_load_b96(rsy, (u & ~1u) * 2u, 0, 0);
+                            d[0] = t[0], d[1] = t[1], d[2] = t[2];
+                        }
+                        uint32_t a[2];
+                        align_units<2>(d, odd, a);
+                        q = u4r{widen16(a[0]), widen16(a[0] >> 16), widen16(a[1]), widen16(a[1] >> 16)};
+                    }
                 };
                 const int ng = (he - h + 3) >> 2;
                 u4r q;
@@ -610,19 +747,27 @@ hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offse
     return launch_rle_fixup(offsets, nblk, ws, ntiles, 0, offsets + nblk, stream);
 }
 
-hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, uint32_t *symbols,
-                           unsigned long long capacity, hipStream_t stream, int num_cus) {
+hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, void *symbols,
+                           int symbol_bytes, unsigned long long capacity, hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
-    hipLaunchKernelGGL(rle_emit_kernel, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, coef, nblk,
-                       offsets, symbols, ntiles, capacity);
+    if (symbol_bytes == 2)
+        hipLaunchKernelGGL(rle_emit_kernel<2>, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, coef,
+                           nblk, offsets, symbols, ntiles, capacity);
+    else
+        hipLaunchKernelGGL(rle_emit_kernel<4>, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, coef,
+                           nblk, offsets, symbols, ntiles, capacity);
     return hipGetLastError();
 }
 
-hipError_t launch_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblk, int16_t *coef,
-                             hipStream_t stream, int num_cus) {
+hipError_t launch_rle_decode(const void *symbols, int symbol_bytes, const uint32_t *offsets, long long nblk,
+                             int16_t *coef, hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
-    hipLaunchKernelGGL(rle_decode_kernel, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, symbols,
-                       offsets, nblk, coef, ntiles);
+    if (symbol_bytes == 2)
+        hipLaunchKernelGGL(rle_decode_kernel<2>, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream,
+                           symbols, offsets, nblk, coef, ntiles);
+    else
+        hipLaunchKernelGGL(rle_decode_kernel<4>, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream,
+                           symbols, offsets, nblk, coef, ntiles);
     return hipGetLastError();
 }
 

@@ -217,34 +217,37 @@ def _all_gather_padded(send, m, group):
 
 def gather_symbols(offsets, symbols, group=None):
     """All-gather every rank's run-length stream (dctq_encode_planes / rle_encode:
-    offsets [n_r + 1], symbols [offsets[n_r]], int32 holding uint32 bit patterns)
-    into the stream of the unsharded input on every rank: (offsets [N + 1],
-    symbols [total]), rank r's offsets shifted by the symbols of ranks < r.
+    offsets [n_r + 1] int32 holding uint32 bit patterns, symbols [offsets[n_r]] --
+    int32 (4-byte symbols) or int16 (the 2-byte format of plans that bound every
+    quantized coefficient by 511)) into the stream of the unsharded input on every
+    rank: (offsets [N + 1], symbols [total]), rank r's offsets shifted by the
+    symbols of ranks < r.
 
     Two collectives: the per-rank sizes (2 int64), then the padded streams --
-    offsets and symbols travel in one buffer, so a shard costs 4 B per block
-    plus 4 B per symbol on the wire instead of 128 B per block."""
+    offsets and symbols travel in one byte buffer, so a shard costs 4 B per block
+    plus 2 or 4 B per symbol on the wire instead of 128 B per block."""
     import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
     n = offsets.numel() - 1
     total = int(offsets[n].item()) & 0xFFFFFFFF
     if symbols.numel() < total:
         raise ValueError("symbols shorter than offsets[n]")
+    if symbols.dtype not in (torch.int16, torch.int32):
+        raise ValueError("symbols must be int16 (2-byte format) or int32 (4-byte format)")
+    w = symbols.element_size()
     dev = offsets.device
     sizes = torch.tensor([n, total], dtype=torch.int64, device=dev)
     allsz = _all_gather_padded(sizes.view(1, 2), 1, group)
     ns = [int(t[0, 0]) for t in allsz]
     tots = [int(t[0, 1]) for t in allsz]
-    m = max(a + b for a, b in zip(ns, tots))
-    send = torch.zeros(m, dtype=torch.int32, device=dev)
-    send[:n] = offsets[:n]
-    send[n:n + total] = symbols[:total]
+    m = max((4 * a + w * b + 3) // 4 * 4 for a, b in zip(ns, tots))
+    send = torch.zeros(m, dtype=torch.uint8, device=dev)
+    send[:4 * n] = offsets[:n].contiguous().view(torch.uint8)
+    send[4 * n:4 * n + w * total] = symbols[:total].contiguous().view(torch.uint8)
     parts = _all_gather_padded(send, m, group)
     offs, syms, base = [], [], 0
     for p, nr, tr in zip(parts, ns, tots):
-        offs.append((p[:nr].to(torch.int64) & 0xFFFFFFFF) + base)
-        syms.append(p[nr:nr + tr])
+        offs.append((p[:4 * nr].view(torch.int32).to(torch.int64) & 0xFFFFFFFF) + base)
+        syms.append(p[4 * nr:4 * nr + w * tr].view(symbols.dtype))
         base += tr
     offs.append(torch.tensor([base], dtype=torch.int64, device=dev))
     return torch.cat(offs).to(torch.int32), torch.cat(syms)

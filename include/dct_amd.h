@@ -96,18 +96,26 @@ int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int 
  * symbols of up to 4 planes.  coef[k] exactly as dctq_forward_quant_planes;
  * blocks numbered plane 0 first, then plane 1, ... (N in total, N < 2^26):
  *   offsets[b]  = first symbol of block b, offsets[N] = total symbols
- *   symbols[..] = the reference's run_length_encode of every block, in order,
- *                 (uint16)value | run << 16 (as dctq_rle_count + dctq_rle_emit
- *                 over the concatenated coefficient planes)
+ *   symbols[..] = the reference's run_length_encode of every block, in order
+ *                 (as dctq_rle_count + dctq_rle_emit over the concatenated
+ *                 coefficient planes), in the plan's symbol format
+ *                 (dctq_plan_symbol_bytes):
+ *                   4 (uint32_t): (uint16_t)value | run << 16;
+ *                   2 (uint16_t): run << 10 | (value & 0x3FF), value in
+ *                     [-511, 511] -- every plan whose quantization table bounds
+ *                     each quantized coefficient there (q <= 90 of the standard
+ *                     table): half the bytes; dctq_rle_decode16 reads it.
  * The symbol count is fused into the forward launch.  Symbols at index >=
  * symbols_capacity are not written; offsets are always complete (compare
  * offsets[N] with the capacity).  symbols == NULL or capacity 0: coefficients
- * and offsets only.  Worst case 64 symbols per block.  workspace:
- * dctq_encode_workspace_bytes(N) bytes. */
+ * and offsets only.  Worst case 64 symbols per block.  symbols 4-byte aligned.
+ * workspace: dctq_encode_workspace_bytes(N) bytes. */
 size_t dctq_encode_workspace_bytes(long long total_blocks);
 int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
-                       uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
+                       uint32_t *offsets, void *symbols, long long symbols_capacity, void *workspace,
                        void *stream);
+/* Bytes per symbol of the plan's encoder output: 2 or 4 (see dctq_encode_planes). */
+int dctq_plan_symbol_bytes(const dctq_plan *plan);
 
 /* Forward DCT only, float coefficients coef[f][by][bx][64]
  * (|coef - dct_forward()| <= 1e-4; computed in fp64, rounded once to fp32). */
@@ -136,7 +144,11 @@ size_t dctq_rle_workspace_bytes(long long nblocks);
 int dctq_rle_count(const int16_t *coef, long long nblocks, uint32_t *offsets, void *workspace, void *stream);
 int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offsets, uint32_t *symbols, void *stream);
 /* The inverse, run_length_decode (src/entropy.c:327-351) + zigzag_to_block
- * (:183-210) of every block: coef[b][64] from symbols[offsets[b] ..). */
+ * (:183-210) of every block: coef[b][64] from symbols[offsets[b] ..).
+ * dctq_rle_decode16: the same from 2-byte symbols (run << 10 | (value & 0x3FF),
+ * a 2-byte plan's dctq_encode_planes output); symbols 4-byte aligned. */
+int dctq_rle_decode16(const uint16_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
+                      void *stream);
 int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
                     void *stream);
 

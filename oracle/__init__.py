@@ -284,6 +284,25 @@ def rle_encode_plane(coef: np.ndarray):
     return off, sym[:total]
 
 
+def pack16(sym: np.ndarray) -> np.ndarray:
+    """4-byte symbols ((uint16)value | run << 16) -> the 2-byte format of plans whose
+    quantized coefficients all lie in [-511, 511]: run << 10 | (value & 0x3FF) (uint16).
+    Test infrastructure: a re-encoding of the reference's (value, run) pairs."""
+    s = np.ascontiguousarray(sym, np.uint32)
+    value = (s & 0xFFFF).astype(np.uint16).view(np.int16).astype(np.int32)
+    run = (s >> 16).astype(np.int32)
+    if s.size and (np.abs(value).max() > 511 or run.max() > 63):
+        raise ValueError("symbol not representable in 2 bytes")
+    return ((run << 10) | (value & 0x3FF)).astype(np.uint16)
+
+
+def unpack16(sym16: np.ndarray) -> np.ndarray:
+    """The 2-byte format -> 4-byte symbols (pack16's inverse)."""
+    u = np.ascontiguousarray(sym16, np.uint16).astype(np.int32)
+    value = ((u & 0x3FF) ^ 0x200) - 0x200
+    return ((value & 0xFFFF) | ((u >> 10) << 16)).astype(np.uint32)
+
+
 def huffman_bits(coeffs) -> int:
     """One 8x8 int block -> the reference pipeline's per-block size: get_encoded_size after
     build_huffman_codes on its RLE symbols (src/entropy.c:261-328, 363-399)."""

@@ -643,6 +643,13 @@ def test_diag_stream_moves_bytes(T, dm):
     assert D.dctq_diag_stream(9, src.data_ptr(), dst.data_ptr(), n, s) != 0
 
 
+def _sym32(sym):
+    """An encoder symbol tensor (int32: 4-byte format, int16: 2-byte format) as 4-byte symbols."""
+    import oracle as O
+    a = sym.cpu().numpy()
+    return O.unpack16(a.view(np.uint16)) if a.dtype == np.int16 else a.view(np.uint32)
+
+
 def _step_blocks(rng, by, bx):
     """Left/right two-level blocks: a quarter of their DCs are exact rounding ties at q50."""
     ab = rng.integers(0, 256, (by, bx, 2), dtype=np.uint8)
@@ -706,7 +713,7 @@ def test_grouped_tie_passes(T, dm):
         assert np.array_equal(T.cat(ec).cpu().numpy(), want), ad
         woff, wsym = O.rle_encode_plane(want)
         assert np.array_equal(off.cpu().numpy().view(np.uint32), woff), ad
-        assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), ad
+        assert np.array_equal(_sym32(sym), wsym), ad
         bits = plan.huffman_bits_planes([g]).cpu().numpy().view(np.uint32)
         assert np.array_equal(bits, O.huffman_bits_plane(want)), ad
 
@@ -1285,6 +1292,9 @@ def test_rle_bit_exact_and_round_trip(T, dm):
         assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym)
         back = dm.rle_decode(sym, off).cpu().numpy()
         assert np.array_equal(back, c)
+        if np.abs(c).max(initial=0) <= 511:  # the 2-byte format (dctq_rle_decode16): every decode path,
+            s16 = T.from_numpy(O.pack16(wsym).view(np.int16).copy()).cuda()  # odd half / lane starts
+            assert np.array_equal(dm.rle_decode(s16, off).cpu().numpy(), c)
     for name, b in g["blocks"].items():  # the reference's own symbols, block by block
         off, sym = dm.rle_encode(T.from_numpy(np.array([b["coeffs"]], np.int16)).cuda())
         s = sym.cpu().numpy().view(np.uint32)
@@ -1306,6 +1316,8 @@ def test_rle_large_planes(T, dm):
     assert np.array_equal(off.cpu().numpy().view(np.uint32), woff)
     assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym)
     assert np.array_equal(dm.rle_decode(sym, off).cpu().numpy(), c.cpu().numpy())
+    s16 = T.from_numpy(O.pack16(wsym).view(np.int16).copy()).cuda()
+    assert np.array_equal(dm.rle_decode(s16, off).cpu().numpy(), c.cpu().numpy())
 
 
 def test_huffman_bits_golden_and_planes(T, dm):
@@ -1509,8 +1521,10 @@ def test_encode_planes_fused(T, dm):
     stack = np.stack([O.synth_plane(90 + f, f % 4, 40, 24) for f in range(3)])
     sets = [[O.synth_plane(7, 0, 8 * 65, 8 * 9), _step_blocks(rng, 7, 13), O.synth_plane(8, 1, 8, 8), stack],
             [_step_blocks(rng, 21, 37)], [O.synth_plane(9, 3, 8 * 129, 8 * 3), O.synth_plane(10, 2, 64, 64)]]
-    for q, ad in [(50, 0), (50, 1), (90, 0), (10, 1), (100, 0)]:
+    for q, ad in [(50, 0), (50, 1), (90, 0), (91, 0), (10, 1), (100, 0)]:
         plan = dm.Plan(q, ad)
+        # 2-byte symbols exactly when the plan bounds every quantized coefficient by 511
+        assert plan.symbol_bytes == (2 if q <= 90 else 4) == dm.symbol_bytes(q, ad), (q, ad)
         for planes in sets:
             want = np.concatenate([np.concatenate([O.forward_plane(f, q, ad) for f in (p if p.ndim == 3 else [p])])
                                    for p in planes])
@@ -1518,7 +1532,13 @@ def test_encode_planes_fused(T, dm):
             coefs, off, sym = plan.encode_planes([gpu_px(T, p) for p in planes])
             assert np.array_equal(T.cat(coefs).cpu().numpy(), want), (q, ad)
             assert np.array_equal(off.cpu().numpy().view(np.uint32), woff), (q, ad)
-            assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), (q, ad)
+            if plan.symbol_bytes == 2:
+                assert sym.dtype == T.int16
+                assert np.array_equal(sym.cpu().numpy().view(np.uint16), O.pack16(wsym)), (q, ad)
+            else:
+                assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), (q, ad)
+            # and back: the decoder of the stream's format restores every block
+            assert np.array_equal(dm.rle_decode(sym, off).cpu().numpy(), want), (q, ad)
 
 
 def test_encode_capacity_and_large(T, dm):
@@ -1543,7 +1563,9 @@ def test_encode_capacity_and_large(T, dm):
     assert all(T.equal(a, b) for a, b in zip(ecoefs, coefs))
     woff, wsym = dm.rle_encode(T.cat(coefs).contiguous())
     assert T.equal(off, woff)
-    assert T.equal(sym, wsym)
+    assert sym.dtype == T.int16  # q50: 2-byte symbols
+    assert np.array_equal(sym.cpu().numpy().view(np.uint16), O.pack16(wsym.cpu().numpy().view(np.uint32)))
+    assert T.equal(dm.rle_decode(sym, off), T.cat(coefs))
 
 
 def test_randomized_sweep_all_planes_apis(T, dm):
@@ -1584,4 +1606,4 @@ def test_randomized_sweep_all_planes_apis(T, dm):
         woff, wsym = O.rle_encode_plane(np.concatenate(want))
         assert all(np.array_equal(c.cpu().numpy(), wv) for c, wv in zip(ecoefs, want)), ("encode coef", trial)
         assert np.array_equal(off.cpu().numpy().view(np.uint32), woff), ("encode offsets", trial, q, ad)
-        assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), ("encode symbols", trial, q, ad)
+        assert np.array_equal(_sym32(sym), wsym), ("encode symbols", trial, q, ad)

@@ -105,3 +105,29 @@ def test_fp32_inverse_simulation_within_bound(GL, q):
     bound = IB.plan_error(q, *GL)[0]
     assert err <= bound, (q, err, bound)
     assert bound <= 5e-5
+
+
+def test_symbol_format_bound():
+    """dctq_plan_symbol_bytes: 2-byte symbols exactly when the plan bounds every |quantized
+    coefficient| by 511 (128 * L1(D[u]) * L1(D[v]) / Q_uv rounded, Q from
+    src/quantization.c:51-77) -- standard tables q <= 90; and the bound holds on the
+    oracle's forward of blocks built to hit it (each coefficient's sign pattern at +-128/127)."""
+    import dct_amd
+    import oracle as O
+    got = [dct_amd.symbol_bytes(q) for q in range(1, 101)]
+    want = [2 if np.floor(IB.coef_max() / IB.quant_table(q) + 0.5).max() <= 511 else 4 for q in range(1, 101)]
+    assert got == want
+    assert got == [2] * 90 + [4] * 10
+    assert all(dct_amd.symbol_bytes(q, True) == got[q - 1] for q in (1, 50, 90, 91, 100))
+    D = O.dct_matrix(8)
+    blocks = []
+    for u in range(8):
+        for v in range(8):
+            s = np.sign(np.outer(D[u], D[v]))
+            blocks += [np.where(s >= 0, 127, -128) + 128, np.where(s >= 0, -128, 127) + 128]
+    px = np.concatenate([np.concatenate(blocks[i:i + 8], axis=1) for i in range(0, 128, 8)], axis=0).astype(np.uint8)
+    for q in (50, 90, 91, 100):
+        m = int(np.abs(O.forward_plane(px, q, 0).astype(np.int32)).max())
+        assert m <= np.floor(IB.coef_max() / IB.quant_table(q) + 0.5).max()
+        if q <= 90:
+            assert m <= 511

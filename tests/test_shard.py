@@ -102,6 +102,12 @@ def _worker(rank, world, port, q):
         woff, wsym = O.rle_encode_plane(np.concatenate([O.forward_plane(f.numpy(), 50, 0) for f in frames]))
         assert np.array_equal(off.numpy().view(np.uint32), woff), "gathered offsets differ"
         assert np.array_equal(sym.numpy().view(np.uint32), wsym), "gathered symbols differ"
+        # the 2-byte format (plans whose |q| <= 511, dctq_plan_symbol_bytes): same offsets, half the bytes
+        off16, sym16 = shard.gather_symbols(torch.from_numpy(loff.view(np.int32)),
+                                            torch.from_numpy(O.pack16(lsym).view(np.int16).copy()))
+        assert sym16.dtype == torch.int16
+        assert np.array_equal(off16.numpy().view(np.uint32), woff), "gathered offsets differ (2-byte)"
+        assert np.array_equal(sym16.numpy().view(np.uint16), O.pack16(wsym)), "gathered 2-byte symbols differ"
 
         # (4) bench.py's N>1 gather leg (BASELINE configs[3], strong scaling) end to end:
         # shard.strong_gather_leg over a ragged frame split, the oracle standing in for the kernel
