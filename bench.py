@@ -101,6 +101,12 @@ def parse():
     return ap.parse_args()
 
 
+def trace(msg: str) -> None:
+    """One progress line on stderr (DCTQ_BENCH_TRACE=1): which leg a failure came from."""
+    if os.environ.get("DCTQ_BENCH_TRACE") == "1":
+        print(f"[bench rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
 def spawn_ranks(n: int) -> int:
     """`--gpus N` (N > 1) with no launcher around this process: start N copies of
     this command as child processes, one per GPU, with the environment
@@ -1000,24 +1006,30 @@ def main():
         nk = (C_W // 8) * (C_H // 8)
         fwd_check = (chroma[0].cpu().numpy(), coef_c[:nk].cpu().numpy())
 
+    trace("headline done")
     movement = (ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, args.ceiling_rounds)
                 if args.ceiling_rounds > 0 and not args.per_plane else None)
 
     gather = band = None
     if dist_on and args.gather_steps > 0:
+        trace("gather leg")
         gather = gather_leg(args, plan, world, rank, dev)
+        trace("band leg")
         band = band_leg(args, plan, luma, chroma, world, dev)
 
     small = small_frame_leg(args, plan, dev) if world == 1 and not args.no_cpu else None  # single-GPU config
 
     encode = None
     if args.encode_steps > 0:
+        trace("encode leg")
         encode = encode_leg(args, plan, luma, chroma, world, dev)
 
     round_trip = None
     if args.round_trip_steps > 0:
+        trace("round trip leg")
         round_trip = round_trip_leg(args, plan, luma, chroma, world, rank, dev)
 
+    trace("legs done")
     total_blocks = world * (nblk_y + nblk_c) * args.steps
     value = total_blocks / el
     traffic, traffic_note = traffic_for(args, launches)

@@ -222,6 +222,8 @@ int dctq::plane_args(const dctq_plane *s, dctq::PlaneArgs *a) {
     a->nblk = (int)tot;
     a->div_bw = dctq::make_fastdiv((uint32_t)bw);
     a->div_frame = dctq::make_fastdiv((uint32_t)per);
+    const long long span = (s->nframes - 1) * s->frame_stride + (s->height - 1) * s->stride + s->width;
+    a->span = span < 0xFFFFFFFFll ? (uint32_t)span : 0u;
     return DCTQ_OK;
 }
 

@@ -118,6 +118,7 @@ struct PlaneArgs {
     int nblk_frame;     // blocks per frame
     int nblk;           // total blocks (all frames), < 2^31
     FastDiv div_bw, div_frame;  // by bw and by nblk_frame
+    uint32_t span;      // bytes from src to one past the last pixel when < 2^32, else 0 (load_rows<true>)
 };
 
 // Up to kMaxPlanes planes (e.g. Y, Cb, Cr) processed by ONE forward launch.

@@ -121,6 +121,10 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
 
 // Pixel rows are read exactly once: non-temporal loads (+8.7 % on the memory
 // ceiling of this stream, profiles/r01/valu_issue_rates.md).
+// BUF: through a buffer descriptor over the plane (p.span bytes from p.src) when
+// the plane spans < 4 GiB: an address VGPR that went wrong then reads zeros
+// instead of faulting the device (the fused round trip).
+template <bool BUF = false>
 __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 (&rows)[8]) {
     if (DCTQ_ABLATE & 64) {  // diagnostic: opaque synthetic rows, no memory traffic
 #pragma unroll
@@ -132,6 +136,19 @@ __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 
         return;
     }
     const uint8_t *px = block_ptr(p, n < (uint32_t)p.nblk ? n : 0);
+    if constexpr (BUF) {
+        if (p.span) {  // kernel argument: wave-uniform
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.src), (short)0, (int)p.span, 0x00020000);
+            const uint32_t off = (uint32_t)(px - p.src), st = (uint32_t)p.stride;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const u2v t = __builtin_amdgcn_raw_buffer_load_b64(rs, off + r * st, 0, 2 /* nt */);
+                rows[r] = make_uint2(t.x, t.y);
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
 #if DCTQ_LOAD_NT
@@ -678,11 +695,11 @@ __device__ __forceinline__ void retire_stores() { __builtin_amdgcn_s_waitcnt(0x0
 #ifndef DCTQ_SKIP_TAIL_PF
 #define DCTQ_SKIP_TAIL_PF 1
 #endif
-template <bool SKIP = true>
+template <bool SKIP = true, bool BUF = false>
 __device__ __forceinline__ void prefetch_batch(const PlaneSet &ps, uint32_t gn, int lane, uint2 (&nxt)[8]) {
     if (SKIP && DCTQ_SKIP_TAIL_PF && gn >= ps.first[ps.n]) return;  // wave-uniform
     const int kn = plane_of(ps, gn);
-    load_rows(ps.pl[kn], (gn - first_of(ps, kn)) * 64 + lane, nxt);
+    load_rows<BUF>(ps.pl[kn], (gn - first_of(ps, kn)) * 64 + lane, nxt);
 }
 
 }  // namespace dctq

@@ -32,6 +32,10 @@ namespace dctq {
 // step (round 3); the wide rounds spill at these kernels' 128-VGPR bound.
 constexpr bool kRtGroup8 = true;
 constexpr int kRtWide = 0;
+#ifndef DCTQ_RT_BUF_ROWS
+#define DCTQ_RT_BUF_ROWS 1
+#endif
+constexpr bool kRtBufRows = DCTQ_RT_BUF_ROWS;  // pixel rows through a plane-bounded buffer descriptor (load_rows)
 
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
 
@@ -145,6 +149,9 @@ __device__ __forceinline__ void swap_halves_f(float &x, float &y) {
 // 32-63, both scale rows in SGPR pairs: two exec-masked v_pk_mul_f32 per pair (a
 // per-lane select of the factor costs 2 v_mov + 1 v_cndmask per value).  The wave
 // is fully active here; exec is saved and restored inside the block.
+#ifndef DCTQ_RT_SCALE_ASM
+#define DCTQ_RT_SCALE_ASM 1  // 0: a per-lane select of the scale pair instead (A/B and fault-isolation switch)
+#endif
 typedef const __attribute__((address_space(4))) uint64_t ConstPair;
 __device__ __forceinline__ void half_wave_scale_f32(f2 (&v)[4], ConstPair *lo, ConstPair *hi) {
     uint64_t save;
@@ -171,8 +178,15 @@ __device__ __forceinline__ void inverse_half_f32(const DevTables *__restrict__ d
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = f2{(float)(int)(int16_t)(w[k] & 0xFFFFu), (float)((int)w[k] >> 16)};
         // row r of the half-wave: row r (lanes 0-31) or r + 4 (lanes 32-63) of the block
+#if DCTQ_RT_SCALE_ASM
         half_wave_scale_f32(x, reinterpret_cast<ConstPair *>(&tp->iscale32[8 * r]),
                             reinterpret_cast<ConstPair *>(&tp->iscale32[8 * (r + 4)]));
+#else
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            x[k] = x[k] * (h ? f2{tp->iscale32[8 * (r + 4) + 2 * k], tp->iscale32[8 * (r + 4) + 2 * k + 1]}
+                             : f2{tp->iscale32[8 * r + 2 * k], tp->iscale32[8 * r + 2 * k + 1]});
+#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             v[r][2 * k] = x[k].x;
@@ -216,7 +230,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
     const uint32_t step = gridDim.x * kWaves;
     uint32_t g = blockIdx.x * kWaves + wv;
     uint2 nxt[8];
-    prefetch_batch(ps, g, lane, nxt);
+    prefetch_batch<true, kRtBufRows>(ps, g, lane, nxt);
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
     uint32_t exact_count = 0;
@@ -229,7 +243,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        prefetch_batch<false>(ps, g + step, lane, nxt);
+        prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));

@@ -502,6 +502,12 @@ def test_stash_captured_launch_survives_grow(T, dm):
     assert L.dctq_diag_stream_stash_bytes(C.c_void_p(s.cuda_stream)) == 0
 
 
+def _tail(err: str) -> str:
+    """A failed bench's stderr: its progress lines (DCTQ_BENCH_TRACE) and the end."""
+    marks = [ln for ln in err.splitlines() if ln.startswith("[bench rank") or "Error" in ln or "error:" in ln]
+    return "\n".join(marks[-40:]) + "\n...\n" + err[-2000:]
+
+
 def test_bench_gpus2_gloo(T, dm):
     """bench.py --gpus 2 with no launcher forms a 2-rank world by itself (its
     children share this box's one GPU over gloo, as a rehearsal of the driver's
@@ -514,11 +520,12 @@ def test_bench_gpus2_gloo(T, dm):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                             "MASTER_PORT")}
+    env["DCTQ_BENCH_TRACE"] = "1"
     cmd = [sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--steps", "2", "--warmup", "1",
            "--no-cpu", "--frames", "2", "--total-frames", "4", "--gather-steps", "2", "--round-trip-steps", "1",
            "--encode-steps", "1", "--ceiling-rounds", "0", "--prewarm-ms", "0"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _tail(r.stderr)
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
@@ -539,7 +546,7 @@ def test_bench_gpus2_gloo(T, dm):
     # ... and a wrong shard offset shared by both shapes fails it (both shapes still agree)
     cmd_f = cmd + ["--gather-fault", "offset", "--round-trip-steps", "0", "--encode-steps", "0"]
     r = subprocess.run(cmd_f, cwd=root, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _tail(r.stderr)
     g = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])["gather"]
     assert g["fault_injected"] == "offset" and g["methods_gather_the_same"] is True, g
     assert g["gathered_equals_unsharded"] is False, g
@@ -560,7 +567,7 @@ def test_dist_legs_rccl_one_rank(T, dm):
            "--total-frames", "2", "--gather-steps", "2", "--round-trip-steps", "0", "--encode-steps", "1",
            "--ceiling-rounds", "0", "--prewarm-ms", "0"]
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _tail(r.stderr)
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["config"]["world_size"] == 1 and d["n_gpus"] == 1
     g, b, e = d["gather"], d["band"], d["encode"]
@@ -588,7 +595,7 @@ def test_bench_json_contract(T, dm):
     cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--frames", "2", "--cpu-seconds", "2",
            "--ceiling-rounds", "1", "--round-trip-steps", "1", "--encode-steps", "1", "--prewarm-ms", "20"]
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _tail(r.stderr)
     lines = [x for x in r.stdout.strip().splitlines() if x.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
     d = json.loads(lines[0])
