@@ -73,9 +73,13 @@ __device__ __forceinline__ void half_wave_scale(double (&v)[8], ConstDouble *lo,
 // waterfall loop (the fused round trip's second half did).
 __device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane, char *dst, uint32_t nbytes) {
     const uint64_t d = reinterpret_cast<uint64_t>(dst);
-    dst = reinterpret_cast<char *>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d >> 32)) << 32) |
-                                   __builtin_amdgcn_readfirstlane((uint32_t)d));
-    nbytes = __builtin_amdgcn_readfirstlane(nbytes);
+    // __builtin_amdgcn_readfirstlane returns int: each half goes back through uint32_t,
+    // or the low half is sign-extended into the high one (an address with bit 31 set
+    // became 0xFFFFFFFF'xxxxxxxx -- the round-5 device faults, profiles/r05/INDEX.md)
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(d >> 32));
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)d);
+    dst = reinterpret_cast<char *>(((uint64_t)hi << 32) | (uint64_t)lo);
+    nbytes = (uint32_t)__builtin_amdgcn_readfirstlane(nbytes);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nbytes, 0x00020000);
     const char *base = reinterpret_cast<const char *>(stage) + wv * 32 * kPitchP;
     u4p val[8];

@@ -252,11 +252,8 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
         int32_t var_num;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
-        // vmcnt(0): the previous batch's recon stores AND this batch's prefetch before any LDS
-        // read.  Not vmcnt(8) with the prefetch issued here instead (round 5): a VMEM
-        // instruction may read its address VGPRs as late as a store reads its data, and the
-        // tie pass's LDS loads then landed in the in-flight prefetch's address registers
-        // (an illegal address on the full-size test, profiles/r05/INDEX.md)
+        // vmcnt(0): the previous batch's recon stores (store-data hazard) and this
+        // batch's prefetch before any LDS read
         retire_stores();
         const uint32_t ne =
             resolve_ties_compact<ADAPTIVE, kRtGroup8, kRtWide>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);

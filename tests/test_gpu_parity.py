@@ -953,6 +953,52 @@ def test_round_trip_inverse_fp32_within_bound(T, dm):
                 assert np.array_equal(got, got64), q
 
 
+def _at_low_word(buf, low, nbytes):
+    """A 256-B aligned slice of `buf` (uint8, > 4 GiB) whose device address has low 32
+    bits >= `low` at its start (wrapping past 2^32 if nbytes runs over)."""
+    off = (low - buf.data_ptr()) % (1 << 32)
+    off = (off + 255) // 256 * 256
+    assert off + nbytes <= buf.numel()
+    return buf[off:off + nbytes]
+
+
+@pytest.mark.parametrize("low", [0x80000000, 0xFFFF0000])
+def test_outputs_at_addresses_with_bit31(T, dm, low):
+    """Outputs placed where the device address's low word has bit 31 set (0x80000000..)
+    or runs over a 4 GiB line (0xFFFF0000..): the paired-lane kernels' stores (store_stage:
+    round trip recon, dctq_inverse, dctq_forward_float) and the coefficient stores must
+    land exactly where the same launch writes into an ordinary allocation.  The round-5
+    device faults came from store_stage sign-extending the low half of its readfirstlane'd
+    base address (profiles/r05/INDEX.md)."""
+    luma = dm.synth(4242, "uniform", 1920, 1080, 2)
+    chroma = dm.synth(4343, "uniform", 960, 536, 4)
+    nb = [px.shape[0] * (px.shape[1] // 8) * (px.shape[2] // 8) for px in (luma, chroma)]
+    buf = T.empty((1 << 32) + (64 << 20), dtype=T.uint8, device="cuda")
+    for q, ad in [(50, 0), (50, 1)]:
+        plan = dm.Plan(q, ad)
+        (c0, c1), (r0, r1) = plan.round_trip_planes([luma, chroma])
+        co = [_at_low_word(buf, low, n * 128).view(T.int16).view(n, 64) for n in nb]
+        re = [_at_low_word(buf, low + (32 << 20), n * 256).view(T.float32).view(n, 64) for n in nb]
+        plan.round_trip_planes([luma, chroma], outs=co, recons=re)
+        assert T.equal(co[0], c0) and T.equal(co[1], c1), (q, ad)
+        assert T.equal(re[0], r0) and T.equal(re[1], r1), (q, ad)
+        vn = T.empty(nb[0], dtype=T.int32, device="cuda")
+        plan.forward_quant(luma, var_num=vn)
+        want = plan.inverse(c0, var_num=vn)
+        got = _at_low_word(buf, low, nb[0] * 256).view(T.float32).view(nb[0], 64)
+        plan.inverse(c0, var_num=vn, out=got)
+        assert T.equal(got, want), (q, ad)
+        wf = plan.forward_float(luma)
+        gf = _at_low_word(buf, low + (16 << 20), nb[0] * 256).view(T.float32).view(nb[0], 64)
+        plan.forward_float(luma, out=gf)
+        assert T.equal(gf, wf), (q, ad)
+        gq = _at_low_word(buf, low, nb[0] * 128).view(T.int16).view(nb[0], 64)
+        plan.forward_quant(luma, out=gq)
+        assert T.equal(gq, c0), (q, ad)
+    del buf
+    T.cuda.empty_cache()
+
+
 def test_round_trip_exact_count_matches_forward(T, dm):
     """The fused kernel resolves ties in place; it recomputes exactly the
     coefficients the forward kernel sends to its deferred queue."""
