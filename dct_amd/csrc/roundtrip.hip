@@ -36,6 +36,9 @@ constexpr int kRtWide = 0;
 #define DCTQ_RT_BUF_ROWS 1
 #endif
 constexpr bool kRtBufRows = DCTQ_RT_BUF_ROWS;  // pixel rows through a plane-bounded buffer descriptor (load_rows)
+#ifndef DCTQ_RT_LATE_PF
+#define DCTQ_RT_LATE_PF 0  // A/B: the next batch's rows requested after the forward, vmcnt(8) before the tie pass
+#endif
 
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
 
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
+        if (!DCTQ_RT_LATE_PF) prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
@@ -252,9 +255,16 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
         int32_t var_num;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
-        // vmcnt(0): the previous batch's recon stores (store-data hazard) and this
-        // batch's prefetch before any LDS read
-        retire_stores();
+        if (DCTQ_RT_LATE_PF) {
+            // the previous batch's recon stores are older than these 8 loads (one in-order
+            // counter): vmcnt(8) retires them before any LDS read and leaves the rows in flight
+            prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
+            __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+        } else {
+            // vmcnt(0): the previous batch's recon stores (store-data hazard) and this
+            // batch's prefetch before any LDS read
+            retire_stores();
+        }
         const uint32_t ne =
             resolve_ties_compact<ADAPTIVE, kRtGroup8, kRtWide>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
