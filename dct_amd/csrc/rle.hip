@@ -8,11 +8,14 @@
 // block has exactly 1 + nnz(first 63 zigzag elements) symbols.  Blocks are
 // concatenated in order.  Two symbol formats (round 5):
 //   W = 4 (uint32): (uint16)value | run << 16 -- any int16 value;
-//   W = 2 (uint16): run << 10 | (value & 0x3FF) -- |value| <= 511, which a plan
-//         guarantees when its Q table bounds every quantized coefficient there
+//   W = 2 (uint16): (run & 63) << 10 | (value & 0x3FF) -- |value| <= 511, which a
+//         plan guarantees when its Q table bounds every quantized coefficient there
 //         (api.hip symbol_bytes; q <= 90 of the standard table): 2 B per symbol,
 //         so dense noise's 45.7 symbols per block take 91 B instead of 183 B --
 //         less than the 128 B of int16 coefficients they shrink.
+//         Runs are 0..63 except in the one symbol of an all-zero block, (0, 64),
+//         which packs to 0x0000: no other symbol does (a zero value only ends a
+//         block, and then its run counts itself, >= 1).
 //
 // Layout choices (DESIGN.md "RLE"): one WAVE per block -- lane i holds zigzag
 // element i, so "nonzero" is a ballot, a symbol's index is mbcnt of that ballot,
@@ -38,13 +41,13 @@ constexpr int kRleThreads = 64 * kRleWaves;
 template <int W>
 __device__ __forceinline__ uint32_t pack_sym(uint32_t v16, uint32_t r) {
     if constexpr (W == 4) return (v16 & 0xFFFFu) | (r << 16);
-    else return (r << 10) | (v16 & 0x3FFu);
+    else return ((r & 63u) << 10) | (v16 & 0x3FFu);  // (0, 64) -> 0x0000
 }
 // ... and back: the run, and the value as int16 bits (sign-extended from 10 bits for W = 2)
 template <int W>
 __device__ __forceinline__ uint32_t sym_run(uint32_t s) {
     if constexpr (W == 4) return s >> 16;
-    else return (s >> 10) & 0x3Fu;
+    else return (s & 0xFFFFu) ? (s >> 10) & 0x3Fu : 64u;
 }
 template <int W>
 __device__ __forceinline__ int16_t sym_value(uint32_t s) {

@@ -101,10 +101,13 @@ int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int 
  *                 coefficient planes), in the plan's symbol format
  *                 (dctq_plan_symbol_bytes):
  *                   4 (uint32_t): (uint16_t)value | run << 16;
- *                   2 (uint16_t): run << 10 | (value & 0x3FF), value in
- *                     [-511, 511] -- every plan whose quantization table bounds
- *                     each quantized coefficient there (q <= 90 of the standard
- *                     table): half the bytes; dctq_rle_decode16 reads it.
+ *                   2 (uint16_t): (run & 63) << 10 | (value & 0x3FF), value
+ *                     in [-511, 511] -- every plan whose quantization table
+ *                     bounds each quantized coefficient there (q <= 90 of the
+ *                     standard table): half the bytes; dctq_rle_decode16 reads
+ *                     it.  Runs are 0..63 except the one symbol of an all-zero
+ *                     block, (value 0, run 64), which is 0x0000 (no other
+ *                     symbol is: a zero value only ends a block, with run >= 1).
  * The symbol count is fused into the forward launch.  Symbols at index >=
  * symbols_capacity are not written; offsets are always complete (compare
  * offsets[N] with the capacity).  symbols == NULL or capacity 0: coefficients
@@ -145,8 +148,9 @@ int dctq_rle_count(const int16_t *coef, long long nblocks, uint32_t *offsets, vo
 int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offsets, uint32_t *symbols, void *stream);
 /* The inverse, run_length_decode (src/entropy.c:327-351) + zigzag_to_block
  * (:183-210) of every block: coef[b][64] from symbols[offsets[b] ..).
- * dctq_rle_decode16: the same from 2-byte symbols (run << 10 | (value & 0x3FF),
- * a 2-byte plan's dctq_encode_planes output); symbols 4-byte aligned. */
+ * dctq_rle_decode16: the same from 2-byte symbols ((run & 63) << 10 | (value &
+ * 0x3FF), 0x0000 = (0, 64); a 2-byte plan's dctq_encode_planes output);
+ * symbols 4-byte aligned. */
 int dctq_rle_decode16(const uint16_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
                       void *stream);
 int dctq_rle_decode(const uint32_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,

@@ -286,21 +286,26 @@ def rle_encode_plane(coef: np.ndarray):
 
 def pack16(sym: np.ndarray) -> np.ndarray:
     """4-byte symbols ((uint16)value | run << 16) -> the 2-byte format of plans whose
-    quantized coefficients all lie in [-511, 511]: run << 10 | (value & 0x3FF) (uint16).
+    quantized coefficients all lie in [-511, 511]: (run & 63) << 10 | (value & 0x3FF)
+    (uint16).  Runs reach 64 only in the single symbol of an all-zero block, (0, 64)
+    (src/entropy.c:231-233: the last element's run counts itself), which becomes 0x0000 --
+    a code no other symbol has (a zero value only ends a block, with run >= 1).
     Test infrastructure: a re-encoding of the reference's (value, run) pairs."""
     s = np.ascontiguousarray(sym, np.uint32)
     value = (s & 0xFFFF).astype(np.uint16).view(np.int16).astype(np.int32)
     run = (s >> 16).astype(np.int32)
-    if s.size and (np.abs(value).max() > 511 or run.max() > 63):
+    if s.size and (np.abs(value).max() > 511 or run.max() > 64 or ((run == 64) & (value != 0)).any()
+                   or ((run == 0) & (value == 0)).any()):
         raise ValueError("symbol not representable in 2 bytes")
-    return ((run << 10) | (value & 0x3FF)).astype(np.uint16)
+    return (((run & 63) << 10) | (value & 0x3FF)).astype(np.uint16)
 
 
 def unpack16(sym16: np.ndarray) -> np.ndarray:
-    """The 2-byte format -> 4-byte symbols (pack16's inverse)."""
+    """The 2-byte format -> 4-byte symbols (pack16's inverse; 0x0000 = (0, 64))."""
     u = np.ascontiguousarray(sym16, np.uint16).astype(np.int32)
     value = ((u & 0x3FF) ^ 0x200) - 0x200
-    return ((value & 0xFFFF) | ((u >> 10) << 16)).astype(np.uint32)
+    run = np.where(u == 0, 64, u >> 10)
+    return ((value & 0xFFFF) | (run << 16)).astype(np.uint32)
 
 
 def huffman_bits(coeffs) -> int:

@@ -953,11 +953,11 @@ def test_round_trip_inverse_fp32_within_bound(T, dm):
                 assert np.array_equal(got, got64), q
 
 
-def _at_low_word(buf, low, nbytes):
-    """A 256-B aligned slice of `buf` (uint8, > 4 GiB) whose device address has low 32
-    bits >= `low` at its start (wrapping past 2^32 if nbytes runs over)."""
+def _at_low_word(buf, low, nbytes, at=0):
+    """A 256-B aligned slice of `buf` (uint8, > 4 GiB) starting `at` bytes past the first
+    address whose low 32 bits are >= `low` (running past 2^32 if it is long enough)."""
     off = (low - buf.data_ptr()) % (1 << 32)
-    off = (off + 255) // 256 * 256
+    off = (off + 255) // 256 * 256 + at
     assert off + nbytes <= buf.numel()
     return buf[off:off + nbytes]
 
@@ -977,8 +977,9 @@ def test_outputs_at_addresses_with_bit31(T, dm, low):
     for q, ad in [(50, 0), (50, 1)]:
         plan = dm.Plan(q, ad)
         (c0, c1), (r0, r1) = plan.round_trip_planes([luma, chroma])
-        co = [_at_low_word(buf, low, n * 128).view(T.int16).view(n, 64) for n in nb]
-        re = [_at_low_word(buf, low + (32 << 20), n * 256).view(T.float32).view(n, 64) for n in nb]
+        at = [0, 9 << 20, 16 << 20, 34 << 20]  # co[0], co[1], re[0], re[1]: disjoint, inside 64 MiB
+        co = [_at_low_word(buf, low, n * 128, a).view(T.int16).view(n, 64) for a, n in zip(at[:2], nb)]
+        re = [_at_low_word(buf, low, n * 256, a).view(T.float32).view(n, 64) for a, n in zip(at[2:], nb)]
         plan.round_trip_planes([luma, chroma], outs=co, recons=re)
         assert T.equal(co[0], c0) and T.equal(co[1], c1), (q, ad)
         assert T.equal(re[0], r0) and T.equal(re[1], r1), (q, ad)
@@ -989,7 +990,7 @@ def test_outputs_at_addresses_with_bit31(T, dm, low):
         plan.inverse(c0, var_num=vn, out=got)
         assert T.equal(got, want), (q, ad)
         wf = plan.forward_float(luma)
-        gf = _at_low_word(buf, low + (16 << 20), nb[0] * 256).view(T.float32).view(nb[0], 64)
+        gf = _at_low_word(buf, low, nb[0] * 256, 16 << 20).view(T.float32).view(nb[0], 64)
         plan.forward_float(luma, out=gf)
         assert T.equal(gf, wf), (q, ad)
         gq = _at_low_word(buf, low, nb[0] * 128).view(T.int16).view(nb[0], 64)

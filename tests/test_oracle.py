@@ -170,6 +170,28 @@ def test_rle_plane_format():
         assert v.tolist() == v2.tolist() and r.tolist() == r2.tolist()
 
 
+def test_two_byte_symbols():
+    """The 2-byte symbol format (include/dct_amd.h): pack16/unpack16 round-trip every symbol
+    of blocks with |q| <= 511 -- runs 0..63, and the all-zero block's (0, 64) as 0x0000, a
+    code no other symbol takes -- and refuse what does not fit."""
+    rng = np.random.default_rng(5)
+    coef = (rng.integers(-511, 512, (400, 64)) * (rng.random((400, 64)) < 0.1)).astype(np.int16)
+    coef[:7] = 0                       # all-zero blocks: one symbol (0, 64)
+    coef[7, 63] = -511                 # a lone last element: run 63
+    coef[8, 62] = 511                  # run 62, then (0, 1)
+    off, sym = O.rle_encode_plane(coef)
+    s16 = O.pack16(sym)
+    assert np.array_equal(O.unpack16(s16), sym)
+    zero_blocks = [b for b in range(coef.shape[0]) if not coef[b].any()]
+    assert (s16 == 0).sum() == len(zero_blocks) >= 7
+    assert all(s16[off[b]] == 0 and off[b + 1] - off[b] == 1 for b in zero_blocks)
+    for bad in ([512, 0], [-512, 0]):
+        c = np.zeros((1, 64), np.int16)
+        c[0, 0] = bad[0]
+        with pytest.raises(ValueError):
+            O.pack16(O.rle_encode_plane(c)[1])
+
+
 def _huffman_golden():
     import json
     import os
