@@ -103,7 +103,20 @@ int main(int argc, char **argv) {
     uint32_t total = 0;
     CHK(dctq_memcpy_dtoh(&total, (const char *)off + (size_t)nblk * 4, 4));
     uint32_t *hs = malloc((size_t)total * 4 + 4);
-    CHK(dctq_memcpy_dtoh(hs, sym, (size_t)total * 4));
+    /* the plan's symbol format (include/dct_amd.h): 2-byte symbols are widened to the
+       4-byte (uint16)value | run << 16 here, so the digest is format-independent */
+    const int symbytes = dctq_plan_symbol_bytes(plan);
+    CHK(dctq_memcpy_dtoh(hs, sym, (size_t)total * symbytes));
+    if (symbytes == 2) {
+        const uint16_t *h16 = (const uint16_t *)hs;
+        for (long long i = (long long)total - 1; i >= 0; --i) {  /* in place, back to front */
+            const uint32_t u = h16[i];
+            const int32_t value = (int32_t)((u & 0x3FFu) ^ 0x200u) - 0x200;
+            const uint32_t run = u ? u >> 10 : 64u;
+            hs[i] = ((uint32_t)value & 0xFFFFu) | run << 16;
+        }
+    }
+    printf("symbol_bytes:%d\n", symbytes);
     uint64_t fs = 1469598103934665603ULL;
     const uint8_t *sb = (const uint8_t *)hs;
     for (long long i = 0; i < (long long)total * 4; ++i) fs = (fs ^ sb[i]) * 1099511628211ULL;

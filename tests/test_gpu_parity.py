@@ -1286,6 +1286,7 @@ def test_c_host_programs(T, dm, blocks, tmp_path):
         for b in wsym.tobytes():
             fs = ((fs ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
         assert int(got["symbols"]) == wsym.size and int(got["symbols_fnv1a"], 16) == fs, (w, h, q, ad)
+        assert int(got["symbol_bytes"]) == dm.symbol_bytes(q, ad) == 2, (w, h, q, ad)
         want_bits = int(O.huffman_bits_plane(np.frombuffer(want, np.int16).reshape(-1, 64)).astype(np.uint64).sum())
         assert int(got["huffman_bits"]) == want_bits, (w, h, q, ad)
 
