@@ -60,18 +60,28 @@ __device__ __forceinline__ void half_wave_scale(double (&v)[8], ConstDouble *lo,
         "s_mov_b32 exec_lo, 0\n\t"
         "v_mul_f64 %0, %0, %17\n\tv_mul_f64 %1, %1, %18\n\tv_mul_f64 %2, %2, %19\n\tv_mul_f64 %3, %3, %20\n\t"
         "v_mul_f64 %4, %4, %21\n\tv_mul_f64 %5, %5, %22\n\tv_mul_f64 %6, %6, %23\n\tv_mul_f64 %7, %7, %24\n\t"
-        "s_mov_b64 exec, %[sv]"
+        "s_mov_b64 exec, %[sv]\n\t"
+        "s_nop 1"  // VALU write -> v_permlane32_swap read (transpose_halves): 2 wait states, ours to pad
         : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
           [sv] "=&s"(save)
         : "s"(lo[0]), "s"(lo[1]), "s"(lo[2]), "s"(lo[3]), "s"(lo[4]), "s"(lo[5]), "s"(lo[6]), "s"(lo[7]),
           "s"(hi[0]), "s"(hi[1]), "s"(hi[2]), "s"(hi[3]), "s"(hi[4]), "s"(hi[5]), "s"(hi[6]), "s"(hi[7]));
 }
 
-// Stage chunk k of the wave's 8 KiB (blocks 4k..4k+3, 16 B per lane) -> HBM.
-// dst and nbytes are wave-uniform; readfirstlane says so to the compiler, which
-// otherwise may keep them in VGPRs under SGPR pressure and wrap every store in a
-// waterfall loop (the fused round trip's second half did).
-__device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane, char *dst, uint32_t nbytes) {
+// Stage chunk k of the wave's 8 KiB (blocks 4k..4k+3, 16 B per lane) -> registers ...
+__device__ __forceinline__ void stage_load(const uint4 *stage, int wv, int lane, u4p (&val)[8]) {
+    const char *base = reinterpret_cast<const char *>(stage) + wv * 32 * kPitchP;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int bl = 4 * k + (lane >> 4);
+        const uint4 t = *reinterpret_cast<const uint4 *>(base + bl * kPitchP + (lane & 15) * 16);
+        val[k] = u4p{t.x, t.y, t.z, t.w};
+    }
+}
+// ... -> HBM as 8 1 KiB stores.  dst and nbytes are wave-uniform; readfirstlane says so
+// to the compiler, which otherwise may keep them in VGPRs under SGPR pressure and wrap
+// every store in a waterfall loop (the fused round trip's second half did).
+__device__ __forceinline__ void stage_store(const u4p (&val)[8], int lane, char *dst, uint32_t nbytes) {
     const uint64_t d = reinterpret_cast<uint64_t>(dst);
     // __builtin_amdgcn_readfirstlane returns int: each half goes back through uint32_t,
     // or the low half is sign-extended into the high one (an address with bit 31 set
@@ -81,16 +91,13 @@ __device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane
     dst = reinterpret_cast<char *>(((uint64_t)hi << 32) | (uint64_t)lo);
     nbytes = (uint32_t)__builtin_amdgcn_readfirstlane(nbytes);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nbytes, 0x00020000);
-    const char *base = reinterpret_cast<const char *>(stage) + wv * 32 * kPitchP;
-    u4p val[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int bl = 4 * k + (lane >> 4);
-        const uint4 t = *reinterpret_cast<const uint4 *>(base + bl * kPitchP + (lane & 15) * 16);
-        val[k] = u4p{t.x, t.y, t.z, t.w};
-    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
+}
+__device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane, char *dst, uint32_t nbytes) {
+    u4p val[8];
+    stage_load(stage, wv, lane, val);
+    stage_store(val, lane, dst, nbytes);
 }
 
 }  // namespace dctq

@@ -32,13 +32,10 @@ namespace dctq {
 // step (round 3); the wide rounds spill at these kernels' 128-VGPR bound.
 constexpr bool kRtGroup8 = true;
 constexpr int kRtWide = 0;
-#ifndef DCTQ_RT_BUF_ROWS
-#define DCTQ_RT_BUF_ROWS 1
-#endif
-constexpr bool kRtBufRows = DCTQ_RT_BUF_ROWS;  // pixel rows through a plane-bounded buffer descriptor (load_rows)
-#ifndef DCTQ_RT_LATE_PF
-#define DCTQ_RT_LATE_PF 0  // A/B: the next batch's rows requested after the forward, vmcnt(8) before the tie pass
-#endif
+// Pixel rows through a plane-bounded buffer descriptor (load_rows<true>): a wrong row
+// address reads zeros instead of faulting; within noise of global loads
+// (profiles/r05/rt_ab_keep_late_rows.log).
+constexpr bool kRtBufRows = true;
 
 static_assert(kThreads == kThreadsP && 64 * kPitch2 == 32 * kPitchP, "forward and inverse share the wave's stage");
 
@@ -150,11 +147,10 @@ __device__ __forceinline__ void swap_halves_f(float &x, float &y) {
 }
 // v[k] (a row's pairs of coefficients) *= lo[k] in lanes 0-31 and *= hi[k] in lanes
 // 32-63, both scale rows in SGPR pairs: two exec-masked v_pk_mul_f32 per pair (a
-// per-lane select of the factor costs 2 v_mov + 1 v_cndmask per value).  The wave
-// is fully active here; exec is saved and restored inside the block.
-#ifndef DCTQ_RT_SCALE_ASM
-#define DCTQ_RT_SCALE_ASM 1  // 0: a per-lane select of the scale pair instead (A/B and fault-isolation switch)
-#endif
+// per-lane select of the factor costs 2 v_mov + 1 v_cndmask per value, and spilled).
+// The wave is fully active here; exec is saved and restored inside the block, and the
+// block ends with the wait states a v_permlane read of its outputs needs (hipcc cannot
+// see inside it).
 typedef const __attribute__((address_space(4))) uint64_t ConstPair;
 __device__ __forceinline__ void half_wave_scale_f32(f2 (&v)[4], ConstPair *lo, ConstPair *hi) {
     uint64_t save;
@@ -165,7 +161,8 @@ __device__ __forceinline__ void half_wave_scale_f32(f2 (&v)[4], ConstPair *lo, C
         "s_mov_b64 exec, %[sv]\n\t"
         "s_mov_b32 exec_lo, 0\n\t"
         "v_pk_mul_f32 %0, %0, %9\n\tv_pk_mul_f32 %1, %1, %10\n\tv_pk_mul_f32 %2, %2, %11\n\tv_pk_mul_f32 %3, %3, %12\n\t"
-        "s_mov_b64 exec, %[sv]"
+        "s_mov_b64 exec, %[sv]\n\t"
+        "s_nop 1"  // VALU write -> v_permlane32_swap read (swap_halves_f next): 2 wait states, ours to pad
         : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), [sv] "=&s"(save)
         : "s"(lo[0]), "s"(lo[1]), "s"(lo[2]), "s"(lo[3]), "s"(hi[0]), "s"(hi[1]), "s"(hi[2]), "s"(hi[3]));
 }
@@ -181,15 +178,8 @@ __device__ __forceinline__ void inverse_half_f32(const DevTables *__restrict__ d
 #pragma unroll
         for (int k = 0; k < 4; ++k) x[k] = f2{(float)(int)(int16_t)(w[k] & 0xFFFFu), (float)((int)w[k] >> 16)};
         // row r of the half-wave: row r (lanes 0-31) or r + 4 (lanes 32-63) of the block
-#if DCTQ_RT_SCALE_ASM
         half_wave_scale_f32(x, reinterpret_cast<ConstPair *>(&tp->iscale32[8 * r]),
                             reinterpret_cast<ConstPair *>(&tp->iscale32[8 * (r + 4)]));
-#else
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            x[k] = x[k] * (h ? f2{tp->iscale32[8 * (r + 4) + 2 * k], tp->iscale32[8 * (r + 4) + 2 * k + 1]}
-                             : f2{tp->iscale32[8 * r + 2 * k], tp->iscale32[8 * r + 2 * k + 1]});
-#endif
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             v[r][2 * k] = x[k].x;
@@ -246,7 +236,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
         const bool valid = b * 64 + lane < (uint32_t)p.nblk;
-        if (!DCTQ_RT_LATE_PF) prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
+        prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
         if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
@@ -255,16 +245,11 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
         int32_t var_num;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, valid, var_num, mlo, mhi);
-        if (DCTQ_RT_LATE_PF) {
-            // the previous batch's recon stores are older than these 8 loads (one in-order
-            // counter): vmcnt(8) retires them before any LDS read and leaves the rows in flight
-            prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
-            __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
-        } else {
-            // vmcnt(0): the previous batch's recon stores (store-data hazard) and this
-            // batch's prefetch before any LDS read
-            retire_stores();
-        }
+        // vmcnt(0): the previous batch's recon stores (store-data hazard) and this
+        // batch's prefetch before any LDS read.  Waiting later (the rows requested after the
+        // forward, vmcnt(8)) or not at all before the recon read-backs (the pending stores' data
+        // kept live instead) measured within noise (profiles/r05/rt_ab_keep_late_rows.log)
+        retire_stores();
         const uint32_t ne =
             resolve_ties_compact<ADAPTIVE, kRtGroup8, kRtWide>(&tab, cur, stage, scr + wv * 64, lane, wv, mlo, mhi);
         if (STATS) exact_count += ne;
@@ -306,7 +291,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
             }
         }
 
-        // ---- 3. paired fp64 inverses, blocks 0-31 then 32-63 of the batch
+        // ---- 3. paired inverses, blocks 0-31 then 32-63 of the batch
         char *mine = wstage + j * kPitchP + h * 128;
         if constexpr (INV32) inverse_half_f32(dev, qa, h, mine);
         else inverse_half<ADAPTIVE>(dev, qa, (int32_t)vv[0], h, mine);

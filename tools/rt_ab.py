@@ -90,6 +90,21 @@ for r in range(args.rounds + 1):
         torch.cuda.synchronize()
         if r:
             times[k].append(e0.elapsed_time(e1) / 3 * 1e-3)
+# every entry's outputs against the first entry's (coefficients; recon -- the fp64 inverse
+# differs from the fp32 one within its bound)
+first = None
+for k, fn in runs.items():
+    if k == "flat":
+        continue
+    assert fn() == 0, k
+    torch.cuda.synchronize()
+    snap = ([t.clone() for t in co], [t.clone() for t in rec])
+    if first is None:
+        first = snap
+    same_c = all(torch.equal(a, b) for a, b in zip(snap[0], first[0]))
+    same_r = all(torch.equal(a, b) for a, b in zip(snap[1], first[1]))
+    dr = max(float((a - b).abs().max()) for a, b in zip(snap[1], first[1]))
+    print(f"{k:40s} coef identical {same_c}  recon identical {same_r}  max |d recon| {dr:.3g}")
 base = statistics.median(times[args.entries[0]])
 for k, v in times.items():
     m = statistics.median(v)
