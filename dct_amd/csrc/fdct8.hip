@@ -43,9 +43,6 @@ namespace dctq {
 // the 2-lane rounds spill too, so those instantiations keep one entry per lane.
 constexpr bool kV3Group8 = true;
 constexpr int kV3Wide = 2;
-#ifndef DCTQ_V3_BUF_ROWS
-#define DCTQ_V3_BUF_ROWS 0  // A/B: pixel rows through a plane-bounded buffer descriptor (load_rows<true>)
-#endif
 // fdct8_quant_v3 launches 16 x its resident workgroups (round 4, profiles/r04/forward_grid_sweep.log,
 // one box, interleaved, two passes: x8 424.6 / 424.0 us, x12 417.1 / 416.1, x16 413.3 / 412.1,
 // x24 416.9 / 417.6, x32 424.0 / 421.0, x48 (one batch per wave) 428.4 / 427.4 on the bench step;
@@ -64,7 +61,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
     const uint32_t step = gridDim.x * kFWaves;
     uint32_t g = blockIdx.x * kFWaves + wv;
     uint2 nxt[8];
-    prefetch_batch<true, (bool)DCTQ_V3_BUF_ROWS>(ps, g, lane, nxt);
+    prefetch_batch(ps, g, lane, nxt);
     asm volatile("" : "+v"(nxt[0]), "+v"(nxt[1]), "+v"(nxt[2]), "+v"(nxt[3]), "+v"(nxt[4]), "+v"(nxt[5]),
                  "+v"(nxt[6]), "+v"(nxt[7])::"memory");
     uint32_t resolved = 0;
@@ -76,7 +73,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         uint2 cur[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) cur[r] = nxt[r];
-        prefetch_batch<true, (bool)DCTQ_V3_BUF_ROWS>(ps, gnext, lane, nxt);
+        prefetch_batch(ps, gnext, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);
         int32_t var_num;
         uint32_t mlo, mhi;

@@ -121,10 +121,12 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
 
 // Pixel rows are read exactly once: non-temporal loads (+8.7 % on the memory
 // ceiling of this stream, profiles/r01/valu_issue_rates.md).
-// BUF: through a buffer descriptor over the plane (p.span bytes from p.src) when
-// the plane spans < 4 GiB: an address VGPR that went wrong then reads zeros
-// instead of faulting the device (the fused round trip).
-template <bool BUF = false>
+// BUF (every product kernel): through a buffer descriptor over the plane (p.span
+// bytes from p.src) when the plane spans < 4 GiB: an address that went wrong then
+// reads zeros -- and fails parity -- instead of faulting the device (round 5,
+// profiles/r05/INDEX.md); within noise of global loads on the forward and the round
+// trip (profiles/r05/forward_buf_rows_ab.log, rt_ab_keep_late_rows.log).
+template <bool BUF = true>
 __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 (&rows)[8]) {
     if (DCTQ_ABLATE & 64) {  // diagnostic: opaque synthetic rows, no memory traffic
 #pragma unroll
@@ -695,7 +697,7 @@ __device__ __forceinline__ void retire_stores() { __builtin_amdgcn_s_waitcnt(0x0
 #ifndef DCTQ_SKIP_TAIL_PF
 #define DCTQ_SKIP_TAIL_PF 1
 #endif
-template <bool SKIP = true, bool BUF = false>
+template <bool SKIP = true, bool BUF = true>
 __device__ __forceinline__ void prefetch_batch(const PlaneSet &ps, uint32_t gn, int lane, uint2 (&nxt)[8]) {
     if (SKIP && DCTQ_SKIP_TAIL_PF && gn >= ps.first[ps.n]) return;  // wave-uniform
     const int kn = plane_of(ps, gn);

@@ -884,7 +884,9 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
     const uint32_t nbatch = ps.first[ps.n];
     const uint32_t step = gridDim.x * kHufWaves;
     uint2 cur[8];
-    prefetch_batch(ps, blockIdx.x * kHufWaves + wv, lane, cur);
+    // global row loads here: the buffer-descriptor form (load_rows<true>) costs this
+    // kernel one VGPR spill at its bound
+    prefetch_batch<true, false>(ps, blockIdx.x * kHufWaves + wv, lane, cur);
     for (uint32_t g = blockIdx.x * kHufWaves + wv; g < nbatch; g += step) {
         const int k = plane_of(ps, g);
         const PlaneArgs &p = ps.pl[k];
@@ -906,7 +908,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0))
             (void)resolve_ties_compact<ADAPTIVE, DCTQ_HP_GROUP8, DCTQ_HP_WIDE>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
         wave_sync();
-        prefetch_batch(ps, g + step, lane, cur);  // the rows are dead now; nothing past the last batch
+        prefetch_batch<true, false>(ps, g + step, lane, cur);  // the rows are dead now; nothing past the last batch
         if (nb < 64) {  // blocks past the end are empty
             if (lane >= nb) {
 #pragma unroll

@@ -333,18 +333,26 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
         const unsigned long long room = capacity > o0 ? capacity - o0 : 0ull;
         if (W == 2 && nsym <= kLaneWalkMax) {
             // 2-B symbols: the tile's stream is staged one unit late when it starts at an
-            // odd unit, so LDS dword j is global dword (o0 - pad) / 2 + j; the dwords that
-            // hold one of the tile's units and one of a neighbour's (or one past
-            // `capacity`) are written as that one unit, every other dword whole
+            // odd unit, so LDS dword j is global dword (o0 - pad) / 2 + j.  Whole dwords go
+            // out as b32 through a descriptor that ends at the last whole one; the (at most
+            // two) dwords shared with a neighbour tile or cut by `capacity` are written as
+            // their one unit by lane 0 afterwards (values read with the chunks, before any
+            // store: store-data hazard)
             const uint32_t pad = o0 & 1u;
             if (lane < nb) emit_lane_walk<2>(lt, lt, lane, offv - o0 + pad);
             wave_sync_lds();
             const unsigned long long first = o0 - pad;  // even: the descriptor base is 4-B aligned
             const unsigned long long cap = capacity > first ? capacity - first : 0ull;  // units below capacity
             const uint32_t end = (uint32_t)(cap < pad + nsym ? cap : pad + nsym);      // units [pad, end) land
-            const __amdgpu_buffer_rsrc_t rsym = __builtin_amdgcn_make_buffer_rsrc(
-                reinterpret_cast<uint16_t *>(symbols) + first, (short)0, (int)((end + 1u) & ~1u) * 2, 0x00020000);
-            const uint32_t ndw = (end + 1u) >> 1;
+            uint16_t *base16 = reinterpret_cast<uint16_t *>(symbols) + first;
+            const __amdgpu_buffer_rsrc_t rfull =
+                __builtin_amdgcn_make_buffer_rsrc(base16, (short)0, (int)((end & ~1u) * 2u), 0x00020000);
+            const __amdgpu_buffer_rsrc_t redge = __builtin_amdgcn_make_buffer_rsrc(base16, (short)0, (int)(end * 2u),
+                                                                                  0x00020000);
+            const bool head = pad && end > 1u, tail = (end & 1u) && end - 1u >= pad;  // wave-uniform
+            const uint16_t *l16 = reinterpret_cast<const uint16_t *>(lt);
+            const uint32_t uhead = head ? l16[1] : 0u, utail = tail ? l16[end - 1u] : 0u;
+            const uint32_t ndw = end >> 1;  // whole dwords (dword 0 is not one when pad)
 #pragma unroll
             for (int r = 0; r < (int)((kLaneWalkMax / 2 + 1 + 1023) / 1024); ++r) {
                 if (r * 1024 >= (int)ndw) break;
@@ -359,15 +367,14 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
 #pragma unroll
                         for (int j = g; j < g + 4; ++j) {
                             const uint32_t d = (uint32_t)((r * kMaxChunks + j) * 64 + lane);
-                            const bool lo = 2 * d >= pad && 2 * d < end, hi = 2 * d + 1 < end;
-                            if (lo && hi)
-                                __builtin_amdgcn_raw_buffer_store_b32(v[j], rsym, d * 4u, 0, 0);
-                            else if (lo)
-                                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v[j], rsym, d * 4u, 0, 0);
-                            else if (hi)
-                                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)(v[j] >> 16), rsym, d * 4u + 2u, 0, 0);
+                            if (r || j || lane || !pad)  // dword 0 holds a neighbour's unit when pad
+                                __builtin_amdgcn_raw_buffer_store_b32(v[j], rfull, d * 4u, 0, 0);
                         }
                     }
+            }
+            if (lane == 0) {
+                if (head) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)uhead, redge, 2u, 0, 0);
+                if (tail) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)utail, redge, (end - 1u) * 2u, 0, 0);
             }
             continue;
         }
