@@ -396,7 +396,9 @@ def gather_op_name(method):
     """What a gather method runs on this process group's backend (bench JSON 'op' strings)."""
     nccl = dist.get_backend() == "nccl"
     if method == "p2p":
-        return ("RCCL grouped ncclSend/ncclRecv direct pushes (batch_isend_irecv)" if nccl
+        # first multi-rank RCCL run of this shape: its own gathered_equals_unsharded is the check
+        return ("RCCL grouped ncclSend/ncclRecv direct pushes (batch_isend_irecv; unverified on hardware before "
+                "this run, see gathered_equals_unsharded)" if nccl
                 else f"{dist.get_backend()} isend/irecv direct pushes (batch_isend_irecv)")
     return "RCCL all_gather_into_tensor" if nccl else f"{dist.get_backend()} all_gather"
 
