@@ -101,6 +101,23 @@ def parse():
     return ap.parse_args()
 
 
+class _StdoutToStderr:
+    """fd 1 -> fd 2 for the duration: gloo's C++ rendezvous prints "[Gloo] Rank r is connected
+    ..." to stdout, and rank 0's stdout must carry the one JSON line only."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
 def trace(msg: str) -> None:
     """One progress line on stderr (DCTQ_BENCH_TRACE=1): which leg a failure came from."""
     if os.environ.get("DCTQ_BENCH_TRACE") == "1":
@@ -164,7 +181,8 @@ def spawn_ranks(n: int) -> int:
 def launch_check(args) -> None:
     """--launch-check: each rank joins a gloo group over the env rendezvous and
     contributes its rank; rank 0 prints the world it saw.  No GPU."""
-    dist.init_process_group("gloo")
+    with _StdoutToStderr():
+        dist.init_process_group("gloo")
     t = torch.tensor([dist.get_rank()], dtype=torch.int64)
     dist.all_reduce(t)
     if dist.get_rank() == 0:
@@ -929,10 +947,11 @@ def main():
     if dist_on:
         local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share a GPU
         torch.cuda.set_device(local)
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
+        with _StdoutToStderr():
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(args.backend)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
     if dist_on:

@@ -28,8 +28,8 @@ def test_gpus_flag_spawns_the_ranks(n):
     r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--launch-check"], cwd=ROOT, env=_env(),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
-    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout  # gloo's rendezvous chatter goes to stderr
     d = json.loads(lines[0])
     assert d == {"n_gpus": n, "world_size": n, "rank_sum": n * (n - 1) // 2, "backend": "gloo"}, d
 

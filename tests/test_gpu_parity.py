@@ -526,8 +526,8 @@ def test_bench_gpus2_gloo(T, dm):
            "--encode-steps", "1", "--ceiling-rounds", "0", "--prewarm-ms", "0"]
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, _tail(r.stderr)
-    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]  # stdout: the one JSON line only
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["world_size"] == 2 and d["config"]["backend"] == "gloo", d["config"]
     g, b = d["gather"], d["band"]
