@@ -278,6 +278,9 @@ LaunchIsolation::LaunchIsolation(const void *stream, int entry) {
             k.entries |= bit;
             return;
         }
+    // a host that creates streams without end: forget them all now and then (each stream's
+    // next first call is isolated again, which only costs that call the lock)
+    if (seen.size() >= 64) seen.clear();
     seen.push_back(SeenKey{dev, stream, bit});
 }
 }  // namespace dctq
