@@ -504,8 +504,10 @@ __device__ __forceinline__ void align_units(const uint32_t (&d)[N + 1], uint32_t
     for (int k = 0; k < N; ++k) out[k] = __builtin_amdgcn_alignbit(d[k + 1], d[k], odd * 16u);
 }
 
+// (the 2-byte instantiation asks for 7 waves/SIMD: at 8 the register allocator spilled two
+// VGPRs; at 7 it fits in 61, so it still runs 8)
 template <int W>
-__global__ __launch_bounds__(kRleThreads, 8) void rle_decode_kernel(const void *__restrict__ symbols,
+__global__ __launch_bounds__(kRleThreads, W == 4 ? 8 : 7) void rle_decode_kernel(const void *__restrict__ symbols,
                                                                  const uint32_t *__restrict__ offsets, long long nblk,
                                                                  int16_t *__restrict__ coef, long long ntiles) {
     __shared__ u4r wave_lds[kRleWaves][kDecLds / 16];
