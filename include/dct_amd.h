@@ -51,6 +51,8 @@ int dctq_plan_create(int quality, int adaptive, dctq_plan **plan);
 /* Bind an existing reference-style context (block_size must be 8); its
  * quant_matrix VALUES are used, so a caller-modified table is honoured. */
 int dctq_plan_from_context(const QuantContext *qctx, dctq_plan **plan);
+/* Frees the plan's device tables (hipFree, which waits for the device as cudaFree
+ * does); launches that use the plan must have been issued before. */
 void dctq_plan_destroy(dctq_plan *plan);
 
 /* A stack of equally-shaped u8 planes in device memory. */
