@@ -416,6 +416,32 @@ def test_batched_calls_do_not_serialise_and_leave_rand_alone(T, dm):
     T.cuda.synchronize()
 
 
+def test_many_streams_rand_and_results(T, dm):
+    """A host that keeps creating streams: past 64 (device, stream) pairs a thread's
+    list of streams it has launched on is cleared (LaunchIsolation) and each stream's
+    next first call is isolated again -- every result stays bit-exact, and glibc's
+    seed-1 sequence drawn between the launches is undisturbed."""
+    libc = C.CDLL("libc.so.6")
+    libc.rand.restype = C.c_int
+    libc.srand(1)
+    want = [libc.rand() for _ in range(300)]
+    plan = dm.Plan(50, 0)
+    px = dm.synth(4040, "uniform", 256, 128, 1)
+    ref = plan.forward_quant(px)
+    T.cuda.synchronize()
+    libc.srand(1)
+    got, outs, streams = [], [], []
+    for i in range(150):
+        st = T.cuda.Stream()
+        streams.append(st)
+        outs.append(plan.forward_quant(px, stream=st))
+        got.append(libc.rand())
+        got.append(libc.rand())
+    T.cuda.synchronize()
+    assert got == want
+    assert all(T.equal(o, ref) for o in outs)
+
+
 class _PerThreadStream:
     """hipStreamPerThread as a stream argument: one handle value (2), a different real stream per thread."""
     cuda_stream = 2
