@@ -246,6 +246,11 @@ constexpr uint32_t kLaneWalkMax = 0;
 constexpr uint32_t kLaneWalkMax = DCTQ_EMIT_WALK_MAX;  // symbols of a tile the lane-per-block path stages
 static_assert(kLaneWalkMax <= kEmitLds / 4 && kLaneWalkMax <= 2048, "two flush rounds of 1 024");
 #endif
+// 2-byte symbols: every tile fits the staging (64 x 64 symbols + one unit of padding in the
+// 9 KiB), so every tile takes the lane-per-block path -- dense ones too: -5.8 % on the bench's
+// encode step against the wave path above 2 048 (profiles/r05/encode_walk4k_ab.log)
+constexpr uint32_t kLaneWalkMax2 = kLaneWalkMax ? 4096u : 0u;
+static_assert(2 * kLaneWalkMax2 + 2 <= kEmitLds, "2-byte staging (one unit of padding) fits the tile's LDS");
 constexpr int kMaxChunks = 16;  // chunks of 64 symbols per flush round
 
 // A tile whose symbols fit the wave's LDS (natural content: ~6 symbols per
@@ -331,7 +336,7 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
         // 32-bit voffset small (the stream itself may exceed 4 GiB); symbols at or
         // past `capacity` are dropped by num_records
         const unsigned long long room = capacity > o0 ? capacity - o0 : 0ull;
-        if (W == 2 && nsym <= kLaneWalkMax) {
+        if (W == 2 && nsym <= kLaneWalkMax2) {
             // 2-B symbols: the tile's stream is staged one unit late when it starts at an
             // odd unit, so LDS dword j is global dword (o0 - pad) / 2 + j.  Whole dwords go
             // out as b32 through a descriptor that ends at the last whole one; the (at most
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
             const uint32_t uhead = head ? l16[1] : 0u, utail = tail ? l16[end - 1u] : 0u;
             const uint32_t ndw = end >> 1;  // whole dwords (dword 0 is not one when pad)
 #pragma unroll
-            for (int r = 0; r < (int)((kLaneWalkMax / 2 + 1 + 1023) / 1024); ++r) {
+            for (int r = 0; r < (int)((kLaneWalkMax2 / 2 + 1 + 1023) / 1024); ++r) {
                 if (r * 1024 >= (int)ndw) break;
                 if (r) __builtin_amdgcn_s_waitcnt(0x0F70);
                 uint32_t v[kMaxChunks];

@@ -1628,15 +1628,21 @@ def test_encode_capacity_and_large(T, dm):
     forward_quant_planes + rle_encode on the GPU."""
     import oracle as O
     plan = dm.Plan(50, 0)
-    for kind in (0, 1):  # dense tiles (wave-per-block emit) and sparse ones (lane-per-block emit)
+    # dense and sparse tiles at q50, and q90 noise (~62 symbols per block: tiles near the 4 096 the
+    # 2-byte lane-per-block path stages) -- every one through the emit's capacity cuts
+    for q, kind in ((50, 0), (50, 1), (90, 0)):
         px = gpu_px(T, O.synth_plane(12, kind, 256, 128))
+        plan = dm.Plan(q, 0)
         _, off, sym = plan.encode_planes([px])
+        woff, wsym = O.rle_encode_plane(O.forward_plane(O.synth_plane(12, kind, 256, 128), q, 0))
+        assert np.array_equal(off.cpu().numpy().view(np.uint32), woff) and np.array_equal(_sym32(sym), wsym), q
         total = int(off[-1].item())
         tile_end = int(off[64].item())
         for cap in (total // 3, total - 1, tile_end, tile_end + 1, 1):
             _, off2, sym2 = plan.encode_planes([px], capacity=cap)
             assert np.array_equal(off.cpu().numpy(), off2.cpu().numpy())
             assert sym2.numel() == cap and np.array_equal(sym2.cpu().numpy(), sym[:cap].cpu().numpy()), (kind, cap)
+    plan = dm.Plan(50, 0)
     luma = dm.synth(13, "uniform", 3840, 2160, 5)
     chroma = dm.synth(14, "smooth", 1920, 1080, 3)
     ecoefs, off, sym = plan.encode_planes([luma, chroma])

@@ -52,11 +52,11 @@ for r in range(ROUNDS + 1):
         res = fn()
         torch.cuda.synchronize()
         if r == 0:
-            got = out().clone() if out else torch.cat([res[1].view(-1)[:1 + nblk], res[2].view(-1)])
+            got = (out().clone(),) if out else (res[1].clone(), res[2].clone())  # offsets, symbols (int32 or int16)
             if key[0] not in refs:
                 refs[key[0]] = got
             else:
-                assert torch.equal(refs[key[0]], got), f"{key} differs"
+                assert all(torch.equal(a, b) for a, b in zip(refs[key[0]], got)), f"{key} differs"
             continue
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
