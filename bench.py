@@ -73,10 +73,17 @@ def parse():
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed forward+all-gather steps (0 = skip)")
     ap.add_argument("--total-frames", type=int, default=64,
                     help="N>1 gather leg (BASELINE configs[3]): 4K luma frames in total, split over the ranks")
-    ap.add_argument("--gather-fault", default="none", choices=["none", "offset"],
+    ap.add_argument("--gather-fault", default="none", choices=["none", "offset", "p2p-raise", "p2p-stall"],
                     help="tests only: 'offset' makes every rank transform the frames one past its own slice (a "
                          "wrong shard offset shared by both gather shapes), so the gather leg's "
-                         "gathered_equals_unsharded must read false")
+                         "gathered_equals_unsharded must read false; 'p2p-raise' / 'p2p-stall' make the last rank "
+                         "raise before posting its direct pushes / sleep past --dist-timeout first, so its peers' "
+                         "p2p gather times out (the line must still carry the headline and the leg's error)")
+    ap.add_argument("--dist-timeout", type=float, default=90.0,
+                    help="N>1: process-group timeout in seconds (a collective still waiting on a peer after it "
+                         "raises in the caller; the optional legs are fail-soft, class Legs)")
+    ap.add_argument("--leg-deadline", type=float, default=0.0,
+                    help="watchdog bound on each optional leg in seconds (0 = 2 x --dist-timeout + 60)")
     ap.add_argument("--encode-steps", type=int, default=10,
                     help="timed steps of the encoder leg (forward + zigzag/RLE symbols; at N>1 plus the "
                          "symbol-stream all-gather); 0 = skip")
@@ -122,6 +129,116 @@ def trace(msg: str) -> None:
     """One progress line on stderr (DCTQ_BENCH_TRACE=1): which leg a failure came from."""
     if os.environ.get("DCTQ_BENCH_TRACE") == "1":
         print(f"[bench rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+class Report:
+    """Rank 0's one JSON line, filled in as the legs finish and printed exactly
+    once: by main() at the end, or by the leg watchdog (Legs) when a leg outlives
+    its deadline -- then with the headline, every leg that finished and the
+    stuck leg's error.  The headline is measured before any optional leg runs,
+    so no later leg can lose it."""
+
+    def __init__(self, rank: int):
+        import threading
+        self.rank = rank
+        self.out = None
+        self._lock = threading.Lock()
+        self._printed = False
+
+    def emit(self) -> None:
+        with self._lock:
+            if self._printed or self.rank != 0 or self.out is None:
+                return
+            self._printed = True
+            for _ in range(3):  # the watchdog may serialise while the main thread adds a key
+                try:
+                    line = json.dumps(self.out, default=str)
+                    break
+                except RuntimeError:
+                    time.sleep(0.01)
+            else:
+                line = json.dumps(dict(self.out), default=str)
+            print(line, flush=True)
+
+
+class Legs:
+    """Fail-soft runner of bench.py's optional legs (everything after the headline).
+
+    run(name, fn, collective) calls fn() and records legs[name] = {"ok": true,
+    "seconds": ...} or {"error": "..."}; an exception is reported, never raised.
+    A collective leg that fails leaves this rank's process group untrusted (a peer
+    may still be inside the collective it abandoned), so every LATER collective
+    leg on this rank is skipped ({"skipped": ...}) rather than risk a mismatched
+    or hanging collective; a peer that is left waiting for this rank then times
+    out in its own collective (the process group's timeout: gloo's per-operation
+    timeout; for RCCL, TORCH_NCCL_BLOCKING_WAIT=1, which main() sets, makes the
+    waiting call raise in the caller at the timeout instead of a watchdog thread
+    tearing the process down) and skips its later legs the same way.
+
+    A watchdog thread bounds every leg by `deadline_s` (a hang inside a kernel or
+    a collective that no timeout reaches): past it, rank 0 prints the Report with
+    that leg's error and every process exits with status 0 (os._exit: no exec,
+    nothing waits on the stuck stream)."""
+
+    def __init__(self, report: Report, dist_on: bool, deadline_s: float):
+        import threading
+        self.report = report
+        self.dist_on = dist_on
+        self.deadline_s = deadline_s
+        self.status = {}
+        self.poisoned = None
+        self._armed = None
+        self._cv = threading.Condition()
+        threading.Thread(target=self._watch, name="bench-leg-watchdog", daemon=True).start()
+
+    def _watch(self):
+        with self._cv:
+            while True:
+                if self._armed is None:
+                    self._cv.wait()
+                    continue
+                name, t_end = self._armed
+                left = t_end - time.monotonic()
+                if left <= 0:
+                    break
+                self._cv.wait(left)
+        self.status[name] = {"error": f"exceeded its {self.deadline_s:.0f} s deadline (leg watchdog): "
+                                      "the line was printed and the process exited"}
+        print(f"bench.py: leg {name} exceeded {self.deadline_s:.0f} s; printing the line and exiting",
+              file=sys.stderr, flush=True)
+        self.report.emit()
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    def run(self, name: str, fn, collective: bool = True):
+        import traceback
+        if collective and self.dist_on and self.poisoned:
+            self.status[name] = {"skipped": f"after leg {self.poisoned} failed on this rank (its process group "
+                                            "can no longer be trusted)"}
+            trace(f"leg {name}: skipped")
+            return None
+        trace(f"leg {name}")
+        with self._cv:
+            self._armed = (name, time.monotonic() + self.deadline_s)
+            self._cv.notify()
+        t0 = time.perf_counter()
+        try:
+            r = fn()
+            self.status[name] = {"ok": True, "seconds": round(time.perf_counter() - t0, 3)}
+            return r
+        except Exception as e:  # noqa: BLE001 -- recorded in the line, never raised
+            self.status[name] = {"error": f"{type(e).__name__}: {e}"[:800],
+                                 "seconds": round(time.perf_counter() - t0, 3)}
+            print(f"bench.py: leg {name} failed on rank {self.report.rank}:", file=sys.stderr)
+            traceback.print_exc(file=sys.stderr)
+            if collective and self.dist_on:
+                self.poisoned = name
+            return None
+        finally:
+            with self._cv:
+                self._armed = None
+                self._cv.notify()
 
 
 def spawn_ranks(n: int) -> int:
@@ -355,7 +472,44 @@ def round_trip_parity(args, ck):
             "psnr_abs_diff": abs(psnr - ck["psnr"]), "blocks": int(want_c.shape[0])}
 
 
-def band_leg(args, plan, luma, chroma, world, dev, reps=20):
+def inject_p2p_fault(args, world, rank, method):
+    """--gather-fault p2p-raise / p2p-stall: the last rank fails its direct-push
+    gather before posting anything (p2p-stall first sleeps past the process
+    group's timeout), so its peers' grouped send/recv wait on it and time out."""
+    if method != "p2p" or rank != world - 1 or not args.gather_fault.startswith("p2p-"):
+        return
+    if args.gather_fault == "p2p-stall":
+        time.sleep(args.dist_timeout + 10.0)
+    raise RuntimeError(f"injected fault (--gather-fault {args.gather_fault}) on rank {rank}")
+
+
+def merge_methods(first, second, second_method, status):
+    """One gather/band result from its per-method legs: `first` (the all-gather
+    leg's dict, or None if it failed) and `second` (the p2p leg's, or None with
+    the reason in `status`).  The summary flags hold over the methods that ran."""
+    if first is None and second is None:
+        return None
+    base = dict(first if first is not None else second)
+    full0 = base.pop("_full", None)
+    methods = dict(base["methods"])
+    if second is not None and first is not None:
+        methods.update(second["methods"])
+        full1 = second.get("_full")
+        if full0 is not None and full1 is not None:
+            if "methods_gather_the_same" in base:
+                base["methods_gather_the_same"] = bool(torch.equal(full0, full1))
+        for k in ("gathered_equals_unsharded", "own_slice_intact"):
+            if k in base and k in second:
+                base[k] = bool(base[k] and second[k])
+    elif first is not None:
+        methods[second_method] = status or {"error": "did not run"}
+        if "methods_gather_the_same" in base:
+            base["methods_gather_the_same"] = None
+    base["methods"] = methods
+    return base
+
+
+def band_leg(args, plan, luma, chroma, world, dev, methods, reps=20):
     """N>1, the north_star's literal split: ONE 4K 4:2:0 frame (its Y, Cb and Cr
     planes) partitioned across the ranks in block-row bands
     (dct_amd.shard.band_shard), forward DCT+quant of every band in one
@@ -363,7 +517,8 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
     holds the whole frame's coefficients (one collective for the three planes,
     shard.gather_planes; ragged bands padded).  Latency-bound (194 400 blocks per frame); max-over-ranks wall
     time per frame, and a check of the gathered planes against an unsharded
-    forward on this rank."""
+    forward on this rank.  `methods`: the gather shapes this call runs (main()
+    runs the all-gather leg first and the direct pushes as a separate, last leg)."""
     from dct_amd import shard
     # the same frame on every rank (each uses only its band of it)
     y = dct_amd.synth(args.seed + 777, args.kind, luma.shape[-1], luma.shape[-2], 1, device=dev)
@@ -393,7 +548,9 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
     rank = dist.get_rank()
     recv = sum(sum(c) - c[rank] for c in counts) * 128
     by = {}
-    for m in shard.GATHER_METHODS:  # SURVEY 8(e)'s two shapes: the all-gather collective, direct peer pushes
+    for m in methods:  # SURVEY 8(e)'s two shapes: the all-gather collective, direct peer pushes
+        inject_p2p_fault(args, world, rank, m)
+
         def once():
             plan.forward_quant_planes(bands, outs=outs)
             return shard.gather_planes(outs, counts, method=m)  # the three planes in one collective / one group
@@ -402,7 +559,7 @@ def band_leg(args, plan, luma, chroma, world, dev, reps=20):
         by[m] = {"op": gather_op_name(m), "us_per_frame": el / reps * 1e6, "blocks_per_s": nblk * reps / el,
                  "gathered_equals_unsharded": all(bool(torch.equal(f, w)) for f, w in zip(full, want)),
                  "xgmi": shard.xgmi_report(recv, el_g / reps, world)}
-    first = by[shard.GATHER_METHODS[0]]
+    first = by[methods[0]]
     return {"op": f"one 4K 4:2:0 frame in block-row bands over {world} ranks: forward_quant_planes(bands) + "
                   f"{first['op']} of the Y/Cb/Cr coefficient planes", "frames": reps,
             "us_per_frame": first["us_per_frame"], "blocks_per_s": first["blocks_per_s"],
@@ -421,15 +578,20 @@ def gather_op_name(method):
     return "RCCL all_gather_into_tensor" if nccl else f"{dist.get_backend()} all_gather"
 
 
-def gather_leg(args, plan, world, rank, dev):
+def gather_leg(args, plan, world, rank, dev, methods):
     """BASELINE configs[3], strong scaling: --total-frames 4K luma frames (64)
     split over the ranks (shard.split: 8 per GPU at N=8), forward DCT+quant of
     each rank's frames, then the RCCL all-gather of every rank's int16
     coefficient planes onto every rank (shard.strong_gather_leg).  Reports the
     kernel-only aggregate (what the GPUs transform per second together) and the
     end-to-end rate with the exchange, apart: SURVEY 8(e) prices the gather at
-    25-170x the compute, so it is bound by xGMI, not by the kernel."""
+    25-170x the compute, so it is bound by xGMI, not by the kernel.  `methods`:
+    the gather shapes this call runs (main() runs the all-gather first, the
+    direct pushes as the last leg); the gathered tensor rides along as "_full"
+    so merge_methods can compare the shapes."""
     from dct_amd import shard
+    for m in methods:
+        inject_p2p_fault(args, world, rank, m)
     lo, hi = shard.split(args.total_frames, world, rank)
     per = (Y_W // 8) * (Y_H // 8)
     # frame f of synth(seed, n) is made from seed + f, so seeding by the global index of the
@@ -454,7 +616,7 @@ def gather_leg(args, plan, world, rank, dev):
             yield g0 * per, plan.forward_quant(fr)
 
     r = shard.strong_gather_leg(forward, frames, counts, args.gather_steps, dev, torch.cuda.synchronize,
-                                unsharded=unsharded)
+                                methods=methods, unsharded=unsharded)
     local = r["local"]
     off = sum(counts[:rank])
     n = r["blocks_per_step"] * r["steps"]
@@ -470,7 +632,7 @@ def gather_leg(args, plan, world, rank, dev):
     # every rank checked its own copy: the leg passes only if all of them hold the unsharded result
     ok = torch.tensor([int(all(v["gathered_equals_unsharded"] for v in by.values()))], device=dev)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    first_m = by[shard.GATHER_METHODS[0]]
+    first_m = by[methods[0]]
     return {"op": f"{args.total_frames} 4K luma frames split over {world} ranks: forward_quant + {first_m['op']} of "
                   "the int16 coefficient planes (BASELINE configs[3])", "scaling": "strong", "world_size": world,
             "frames_total": args.total_frames, "frames_this_rank": hi - lo, "steps": r["steps"],
@@ -478,7 +640,7 @@ def gather_leg(args, plan, world, rank, dev):
             "blocks_per_s": first_m["blocks_per_s"], "ms_per_step": first_m["ms_per_step"],
             "bytes_received_per_rank": recv, "own_slice_intact": all(v["own_slice_intact"] for v in by.values()),
             "methods_gather_the_same": same, "gathered_equals_unsharded": bool(ok.item()),
-            "fault_injected": args.gather_fault, "xgmi": first_m["xgmi"], "methods": by}
+            "fault_injected": args.gather_fault, "xgmi": first_m["xgmi"], "methods": by, "_full": full0}
 
 
 def small_frame_leg(args, plan, dev):
@@ -612,15 +774,18 @@ def encode_leg(args, plan, luma, chroma, world, dev):
         "blocks_per_s": world * n * args.encode_steps / el_f, "ms_per_step": el_f / args.encode_steps * 1e3,
         "hbm_bytes_per_block": 68,
         "equals_forward_then_huffman_bits": bool(torch.equal(fused_bits, torch.cat(bits)))}
-    if dist.is_initialized():
+    def symbol_gather_leg():
+        """N>1, run by main() among the all-gather legs: encode + the symbol streams all-gathered."""
         def encode_gather():
             encode()
             return shard.gather_symbols(off, sym)  # 4 B per block + sb B per symbol on the wire
         el2 = timed(encode_gather)
-        out.update({"gather_op": "encode + symbol-stream all_gather ("
-                                 + ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()) + ")",
-                    "gather_blocks_per_s": world * n * args.encode_steps / el2,
-                    "gather_ms_per_step": el2 / args.encode_steps * 1e3})
+        return {"gather_op": "encode + symbol-stream all_gather ("
+                             + ("RCCL" if dist.get_backend() == "nccl" else dist.get_backend()) + ")",
+                "gather_blocks_per_s": world * n * args.encode_steps / el2,
+                "gather_ms_per_step": el2 / args.encode_steps * 1e3}
+
+    out["_symbol_gather_leg"] = symbol_gather_leg if dist.is_initialized() else None
     return out
 
 
@@ -945,13 +1110,22 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
     if dist_on:
+        import datetime
+        # a collective still waiting on a peer after --dist-timeout raises in the CALLER (the
+        # optional legs catch it, class Legs): for RCCL that is TORCH_NCCL_BLOCKING_WAIT=1 -- the
+        # waiting call blocks the host until the work completes or the timeout passes, then
+        # throws, and torch creates no watchdog thread that would tear the process down instead
+        # (DESIGN 7); gloo raises at the timeout by itself
+        if args.backend == "nccl":
+            os.environ.setdefault("TORCH_NCCL_BLOCKING_WAIT", "1")
         local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share a GPU
         torch.cuda.set_device(local)
+        timeout = datetime.timedelta(seconds=args.dist_timeout)
         with _StdoutToStderr():
             if args.backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
             else:
-                dist.init_process_group(args.backend)
+                dist.init_process_group(args.backend, timeout=timeout)
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
     if dist_on:
@@ -1020,92 +1194,117 @@ def main():
     avg_launch_bytes = BYTES_PER_BLOCK * (nblk_y + nblk_c) / launches
     achieved = avg_launch_bytes / avg_launch_s / 1e9
 
-    # host copies of one chroma plane and its coefficients: the CPU leg (rank 0, N=1)
+    # host copies of one chroma plane and its coefficients: the CPU leg (rank 0)
     # checks them against the oracle
     fwd_check = None
     if rank == 0:
         nk = (C_W // 8) * (C_H // 8)
         fwd_check = (chroma[0].cpu().numpy(), coef_c[:nk].cpu().numpy())
-
     trace("headline done")
-    movement = (ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, args.ceiling_rounds)
-                if args.ceiling_rounds > 0 and not args.per_plane else None)
 
-    gather = band = None
-    if dist_on and args.gather_steps > 0:
-        trace("gather leg")
-        gather = gather_leg(args, plan, world, rank, dev)
-        trace("band leg")
-        band = band_leg(args, plan, luma, chroma, world, dev)
+    # ---- the line, headline first: every optional leg below only adds to it
+    total_blocks = world * (nblk_y + nblk_c) * args.steps
+    traffic, traffic_note = traffic_for(args, launches)
+    report = Report(rank)
+    out = {
+        "metric": "8x8 macroblocks/sec (DCT+quant); % HBM roofline",
+        "value": total_blocks / el,
+        "unit": "macroblocks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "prewarm": prewarm,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (device splitmix64 frames, kind=%s)" % args.kind,
+        "config": {"workload": f"4K 4:2:0 frame stream (BASELINE configs[2] planes), {F} frames/GPU/step, "
+                               f"forward DCT+quant q{args.quality} adaptive={args.adaptive}, int16 out",
+                   "frames_per_gpu": F, "blocks_per_gpu_step": nblk_y + nblk_c, "quality": args.quality,
+                   "adaptive": args.adaptive, "parallelism": f"frames sharded over {world} GPU(s)",
+                   "world_size": world, "backend": dist.get_backend() if dist_on else None},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
+                     "kernel": dct_amd.forward_kernel(args.quality, args.adaptive,
+                                                      -(-nblk_y // 64) + -(-nblk_c // 64),
+                                                      torch.cuda.get_device_properties(dev).multi_processor_count),
+                     "avg_launch_us": avg_launch_s * 1e6, "launches_per_step": launches,
+                     "bytes_per_launch": avg_launch_bytes, "movement_ceiling": None},
+        "cpu_baseline": None, "parity_check": None, "parity_error": None,
+        "gather": None, "band": None, "round_trip": None, "encode": None, "small_frame": None,
+        "gpu": None, "build": build_record(),
+        "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
+                "reference-order recomputation for guard-band (tie) coefficients",
+    }
+    report.out = out
+    legs = Legs(report, dist_on, args.leg_deadline or 2 * args.dist_timeout + 60.0)
+    out["legs"] = legs.status
 
-    small = small_frame_leg(args, plan, dev) if world == 1 and not args.no_cpu else None  # single-GPU config
-
+    # ---- optional legs, fail-soft (class Legs): this rank's own work first, then the
+    # legs whose steps hold all-gathers, then the direct-push (p2p) legs last
+    if args.ceiling_rounds > 0 and not args.per_plane:
+        out["roofline"]["movement_ceiling"] = legs.run(
+            "ceilings", lambda: ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, args.ceiling_rounds),
+            collective=False)
+    if world == 1 and not args.no_cpu:  # single-GPU config
+        out["small_frame"] = legs.run("small_frame", lambda: small_frame_leg(args, plan, dev), collective=False)
     encode = None
-    if args.encode_steps > 0:
-        trace("encode leg")
-        encode = encode_leg(args, plan, luma, chroma, world, dev)
-
+    if args.encode_steps > 0:  # its timing takes the max over ranks: collective at N>1
+        encode = legs.run("encode", lambda: encode_leg(args, plan, luma, chroma, world, dev))
     round_trip = None
     if args.round_trip_steps > 0:
-        trace("round trip leg")
-        round_trip = round_trip_leg(args, plan, luma, chroma, world, rank, dev)
-
+        round_trip = legs.run("round_trip", lambda: round_trip_leg(args, plan, luma, chroma, world, rank, dev))
+    # host copies for the CPU leg's oracle checks come off the leg results at once: the
+    # line may be printed (watchdog) at any point from here on
+    huf_check = encode["huffman"].pop("_check", None) if encode else None
+    rt_check = round_trip.pop("_check", None) if round_trip else None
+    symbol_gather = encode.pop("_symbol_gather_leg", None) if encode else None
+    out["encode"], out["round_trip"] = encode, round_trip
+    gather_parts, band_parts = {}, {}
+    if dist_on and args.gather_steps > 0:
+        gather_parts["all_gather"] = legs.run(
+            "gather.all_gather", lambda: gather_leg(args, plan, world, rank, dev, ("all_gather",)))
+        band_parts["all_gather"] = legs.run(
+            "band.all_gather", lambda: band_leg(args, plan, luma, chroma, world, dev, ("all_gather",)))
+    if symbol_gather is not None:
+        sg = legs.run("encode.symbol_gather", symbol_gather)
+        encode.update(sg or {"gather_error": legs.status["encode.symbol_gather"]})
+    if dist_on and args.gather_steps > 0:
+        gather_parts["p2p"] = legs.run("gather.p2p", lambda: gather_leg(args, plan, world, rank, dev, ("p2p",)))
+        band_parts["p2p"] = legs.run("band.p2p", lambda: band_leg(args, plan, luma, chroma, world, dev, ("p2p",)))
+        out["gather"] = merge_methods(gather_parts["all_gather"], gather_parts["p2p"], "p2p",
+                                      legs.status.get("gather.p2p"))
+        out["band"] = merge_methods(band_parts["all_gather"], band_parts["p2p"], "p2p",
+                                    legs.status.get("band.p2p"))
+        if out["gather"] is not None:
+            out["gather"].setdefault("fault_injected", args.gather_fault)
     trace("legs done")
-    total_blocks = world * (nblk_y + nblk_c) * args.steps
-    value = total_blocks / el
-    traffic, traffic_note = traffic_for(args, launches)
+
     if rank == 0:
-        huf_check = encode["huffman"].pop("_check", None) if encode else None
-        rt_check = round_trip.pop("_check", None) if round_trip else None
-        cpu, parity = (None, None) if args.no_cpu else cpu_leg(args, world, fwd_check, huf_check, rt_check)
-        if encode and parity is not None:
-            encode["huffman"]["parity_check_chroma0"] = parity.get("huffman")
-        if round_trip and parity is not None and "round_trip" in parity:
-            rp = parity["round_trip"]
-            round_trip["parity"] = rp
-            round_trip["parity_check"] = bool(rp["coef_bit_exact"] and rp["recon_within_1e-4"]
-                                              and rp["psnr_abs_diff"] <= 1e-3)
-        out = {
-            "metric": "8x8 macroblocks/sec (DCT+quant); % HBM roofline",
-            "value": value,
-            "unit": "macroblocks/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "prewarm": prewarm,
-            "ms_per_step": el / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (device splitmix64 frames, kind=%s)" % args.kind,
-            "config": {"workload": f"4K 4:2:0 frame stream (BASELINE configs[2] planes), {F} frames/GPU/step, "
-                                   f"forward DCT+quant q{args.quality} adaptive={args.adaptive}, int16 out",
-                       "frames_per_gpu": F, "blocks_per_gpu_step": nblk_y + nblk_c, "quality": args.quality,
-                       "adaptive": args.adaptive, "parallelism": f"frames sharded over {world} GPU(s)",
-                       "world_size": world, "backend": dist.get_backend() if dist_on else None},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_note,
-                         "kernel": dct_amd.forward_kernel(args.quality, args.adaptive,
-                                                          -(-nblk_y // 64) + -(-nblk_c // 64),
-                                                          torch.cuda.get_device_properties(dev).multi_processor_count),
-                         "avg_launch_us": avg_launch_s * 1e6, "launches_per_step": launches,
-                         "bytes_per_launch": avg_launch_bytes, "movement_ceiling": movement},
-            "cpu_baseline": cpu,
-            "parity_check": parity.get("forward") if parity else None,
-            "parity_error": parity.get("error") if parity else None,
-            "gather": gather,
-            "band": band,
-            "round_trip": round_trip,
-            "encode": encode,
-            "small_frame": small,
-            "gpu": gpu_identity(),
-            "build": build_record(),
-            "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
-                    "reference-order recomputation for guard-band (tie) coefficients",
-        }
-        print(json.dumps(out))
+        if not args.no_cpu:
+            res = legs.run("cpu", lambda: cpu_leg(args, world, fwd_check, huf_check, rt_check), collective=False)
+            cpu, parity = res if res is not None else (None, None)
+            out["cpu_baseline"] = cpu
+            if parity is not None:
+                out["parity_check"], out["parity_error"] = parity.get("forward"), parity.get("error")
+                if encode:
+                    encode["huffman"]["parity_check_chroma0"] = parity.get("huffman")
+                if round_trip and "round_trip" in parity:
+                    rp = parity["round_trip"]
+                    round_trip["parity"] = rp
+                    round_trip["parity_check"] = bool(rp["coef_bit_exact"] and rp["recon_within_1e-4"]
+                                                      and rp["psnr_abs_diff"] <= 1e-3)
+        out["gpu"] = gpu_identity()
+    report.emit()
     if dist_on:
+        if legs.poisoned:
+            # a collective this rank gave up on may still be queued on its stream: leave
+            # without tearing the group down (destroy would wait on it)
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
         dist.destroy_process_group()
 
 

@@ -88,3 +88,119 @@ def test_timed_steady_prewarm_agrees_across_ranks():
     for p, (o, e) in zip(procs, outs):
         assert p.returncode == 0, e[-3000:]
         assert any(x.startswith("OK") for x in o.splitlines()), o
+
+
+_LEGS_WORKER = r"""
+import datetime, json, os, sys, time
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["ROOT"])
+import bench
+mode = os.environ["MODE"]
+dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=5))
+rank, world = dist.get_rank(), dist.get_world_size()
+rep = bench.Report(rank)
+rep.out = {"value": 123.0}
+legs = bench.Legs(rep, True, deadline_s=60.0)
+rep.out["legs"] = legs.status
+
+def all_gather():
+    parts = [torch.empty(4) for _ in range(world)]
+    dist.all_gather(parts, torch.full((4,), float(rank)))
+    return [float(p[0]) for p in parts]
+
+def p2p():  # the last rank fails before posting its push, as bench.py --gather-fault p2p-raise/-stall does
+    if rank == world - 1:
+        if mode == "stall":
+            time.sleep(8.0)
+        raise RuntimeError("injected")
+    buf = torch.empty(4)
+    for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, buf, group_peer=world - 1)]):
+        w.wait()
+    return "received"
+
+t0 = time.time()
+rep.out["ag"] = legs.run("ag", all_gather)
+rep.out["p2p"] = legs.run("p2p", p2p)
+rep.out["after"] = legs.run("after", all_gather)
+rep.out["local"] = legs.run("local", lambda: 7, collective=False)
+rep.out["elapsed"] = time.time() - t0
+print("STATUS", rank, json.dumps(legs.status), flush=True)
+rep.emit()
+sys.stdout.flush()
+os._exit(0)
+"""
+
+
+@pytest.mark.parametrize("mode", ["raise", "stall"])
+def test_legs_fail_soft_p2p_peer(mode):
+    """bench.Legs: at world 2 over gloo, the last rank fails its
+    direct-push leg before posting (raising at once, or after stalling past the
+    process group's 5 s timeout).  Rank 0's grouped receive raises in the caller
+    within the timeout, the leg is recorded as an error on both ranks, the later
+    collective leg is skipped on both (no mismatched collective), the local leg
+    still runs, and rank 0 prints the one line with the headline value."""
+    import socket
+    import time
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    t0 = time.time()
+    procs = [subprocess.Popen([sys.executable, "-c", _LEGS_WORKER], cwd=ROOT, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True,
+                              env=_env(ROOT=ROOT, MODE=mode, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                                       MASTER_PORT=str(port)))
+             for r in range(2)]
+    outs = [p.communicate(timeout=180) for p in procs]
+    assert time.time() - t0 < 120
+    status = {}
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+        for ln in o.splitlines():
+            if ln.startswith("STATUS"):
+                _, r, js = ln.split(" ", 2)
+                status[int(r)] = json.loads(js)
+    lines = [x for x in outs[0][0].splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and not any(x.startswith("{") for x in outs[1][0].splitlines())
+    d = json.loads(lines[0])
+    assert d["value"] == 123.0 and d["ag"] == [0.0, 1.0] and d["p2p"] is None and d["local"] == 7, d
+    assert d["elapsed"] < 30, d
+    for r in (0, 1):
+        s = status[r]
+        assert s["ag"]["ok"] and s["local"]["ok"], (r, s)
+        assert "error" in s["p2p"], (r, s)
+        assert "skipped" in s["after"], (r, s)
+    assert "injected" in status[1]["p2p"]["error"]
+    assert d["legs"] == status[0]
+
+
+_WATCHDOG_WORKER = r"""
+import os, sys, time
+sys.path.insert(0, os.environ["ROOT"])
+import bench
+rep = bench.Report(0)
+rep.out = {"value": 5.0}
+legs = bench.Legs(rep, False, deadline_s=1.5)
+rep.out["legs"] = legs.status
+rep.out["fine"] = legs.run("fine", lambda: 1, collective=False)
+legs.run("stuck", lambda: time.sleep(60), collective=False)
+print("NOT REACHED", flush=True)
+"""
+
+
+def test_legs_watchdog_prints_the_line():
+    """A leg stuck past its deadline (a hang no collective timeout reaches): the
+    watchdog prints the line with the headline, the finished legs and the stuck
+    leg's error, and the process exits 0 without waiting for the leg."""
+    import time
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", _WATCHDOG_WORKER], cwd=ROOT, env=_env(ROOT=ROOT),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert time.time() - t0 < 40
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1 and "NOT REACHED" not in r.stdout, r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] == 5.0 and d["fine"] == 1 and d["legs"]["fine"]["ok"] is True, d
+    assert "deadline" in d["legs"]["stuck"]["error"], d

@@ -577,6 +577,27 @@ def test_bench_gpus2_gloo(T, dm):
     assert g["fault_injected"] == "offset" and g["methods_gather_the_same"] is True, g
     assert g["gathered_equals_unsharded"] is False, g
     assert not any(g["methods"][m]["gathered_equals_unsharded"] for m in ("all_gather", "p2p")), g
+    # a p2p peer that stalls past the process-group timeout and then fails.
+    # The p2p legs run last and fail soft: the line still carries the headline, the all-gather
+    # legs' results and the p2p leg's error, within a bounded time, and every rank exits 0.
+    import time
+    cmd_s = cmd + ["--gather-fault", "p2p-stall", "--dist-timeout", "15", "--round-trip-steps", "0",
+                   "--encode-steps", "1"]
+    t0 = time.time()
+    r = subprocess.run(cmd_s, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, _tail(r.stderr)
+    assert time.time() - t0 < 200
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["roofline"]["frac"] > 0 and d["n_gpus"] == 2, d
+    lg = d["legs"]
+    assert lg["gather.all_gather"]["ok"] and lg["band.all_gather"]["ok"] and lg["encode.symbol_gather"]["ok"], lg
+    assert "error" in lg["gather.p2p"] and "skipped" in lg["band.p2p"], lg
+    g, b = d["gather"], d["band"]
+    assert g["methods"]["all_gather"]["gathered_equals_unsharded"] is True and "error" in g["methods"]["p2p"], g
+    assert b["methods"]["all_gather"]["gathered_equals_unsharded"] is True and "skipped" in b["methods"]["p2p"], b
+    assert d["encode"]["gather_blocks_per_s"] > 0, d["encode"]
 
 
 def test_dist_legs_rccl_one_rank(T, dm):
