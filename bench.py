@@ -703,8 +703,8 @@ def small_frame_leg(args, plan, dev):
 
 
 def encode_leg(args, plan, luma, chroma, world, dev):
-    """the encoder over the frame stream -- dctq_encode_planes
-    (forward + zigzag run-length symbols of reference semantics, the symbol count
+    """the encoder over the frame stream -- dctq_encode_planes16
+    (2-byte symbols, where the plan admits them; else dctq_encode_planes) (forward + zigzag run-length symbols of reference semantics, the symbol count
     fused into the forward launch) -- and at N>1 the all-gather of every rank's
     symbol stream (shard.gather_symbols), end to end, max over ranks.  Reports the
     stream size against the int16 coefficient planes (the bench's uniform input
@@ -723,16 +723,17 @@ def encode_leg(args, plan, luma, chroma, world, dev):
     off = torch.empty(n + 1, dtype=torch.int32, device=dev)
     cap = 64 * n
     sb = plan.symbol_bytes  # 2 when the plan bounds every |quantized coefficient| by 511 (q <= 90)
+    enc = L.dctq_encode_planes16 if sb == 2 else L.dctq_encode_planes  # the opt-in 2-byte format where admitted
     sym = torch.empty(cap, dtype=torch.int16 if sb == 2 else torch.int32, device=dev)
     ws = torch.empty(int(L.dctq_encode_workspace_bytes(n)) // 4 + 1, dtype=torch.int32, device=dev)
     cp = (C.c_void_p * 2)(*[c.data_ptr() for c in coefs])
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def encode():
-        rc = L.dctq_encode_planes(plan._h, descs, 2, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
-                                  C.c_void_p(sym.data_ptr()), cap, C.c_void_p(ws.data_ptr()), stream)
+        rc = enc(plan._h, descs, 2, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
+                 C.c_void_p(sym.data_ptr()), cap, C.c_void_p(ws.data_ptr()), stream)
         if rc:
-            raise RuntimeError(f"dctq_encode_planes rc={rc}")
+            raise RuntimeError(f"dctq_encode_planes{'16' if sb == 2 else ''} rc={rc}")
 
     def timed(fn):
         return timed_steady(fn, args.encode_steps, dev)

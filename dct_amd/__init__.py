@@ -46,6 +46,8 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
         "dctq_round_trip_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, vp], i),
         "dctq_encode_workspace_bytes": ([ll], C.c_size_t),
         "dctq_encode_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp, ll, vp, vp], i),
+        "dctq_encode_planes16": ([vp, C.POINTER(_Plane), i, vp, vp, vp, ll, vp, vp], i),
+        "dctq_abi_version": ([], i),
         "dctq_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
         "dctq_inverse": ([vp, vp, vp, ll, vp, vp], i),
         "dctq_synth": ([C.c_uint64, i, C.POINTER(_Plane), vp], i),
@@ -64,6 +66,9 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
     if diagnostic:
         sig.update({
             "dctq_diag_plan_set_variant": ([vp, i], i),
+            "dctq_diag_forward_quant_planes": ([vp, C.POINTER(_Plane), i, vp, vp, vp], i),
+            "dctq_diag_forward_float": ([vp, C.POINTER(_Plane), vp, vp], i),
+            "dctq_diag_inverse": ([vp, vp, vp, ll, vp, vp], i),
             "dctq_diag_plan_set_num_cus": ([vp, i], i),
             "dctq_diag_plan_set_inverse": ([vp, i], i),
             "dctq_debug_inverse_bound": ([i, i, C.POINTER(i)], C.c_double),
@@ -183,6 +188,8 @@ class Plan:
         self.quality, self.adaptive = quality, bool(adaptive)
         diagnostic = diagnostic or variant is not None or num_cus is not None or inverse is not None
         self._L = diag() if diagnostic else lib()
+        # a forced variant is honoured by the diagnostic entry points only (csrc/dctq_diag.h)
+        self._diag = variant is not None
         h = C.c_void_p()
         self._chk(self._L.dctq_plan_create(int(quality), int(bool(adaptive)), C.byref(h)))
         self._h = h
@@ -224,9 +231,15 @@ class Plan:
         _need(out, nblk * 64, torch.int16, "out", px.device)
         if var_num is not None:
             _need(var_num, nblk, torch.int32, "var_num", px.device)
-        self._chk(self._L.dctq_forward_quant(self._h, C.byref(d), C.c_void_p(out.data_ptr()),
-                                        C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
-                                        _stream_ptr(stream)))
+        vn = C.c_void_p(var_num.data_ptr()) if var_num is not None else None
+        if self._diag:
+            op, vp = (C.c_void_p * 1)(out.data_ptr()), (C.c_void_p * 1)(vn.value) if vn is not None else None
+            self._chk(self._L.dctq_diag_forward_quant_planes(self._h, C.byref(d), 1, C.cast(op, C.c_void_p),
+                                                             C.cast(vp, C.c_void_p) if vp is not None else None,
+                                                             _stream_ptr(stream)))
+        else:
+            self._chk(self._L.dctq_forward_quant(self._h, C.byref(d), C.c_void_p(out.data_ptr()), vn,
+                                                 _stream_ptr(stream)))
         return out
 
     def forward_quant_planes(self, planes, outs=None, var_nums=None, stream=None):
@@ -241,9 +254,9 @@ class Plan:
         _need_planes(outs, var_nums, None, nbs, planes)
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
         vp = (C.c_void_p * n)(*[v.data_ptr() for v in var_nums]) if var_nums is not None else None
-        self._chk(self._L.dctq_forward_quant_planes(self._h, descs, n, C.cast(cp, C.c_void_p),
-                                               C.cast(vp, C.c_void_p) if vp is not None else None,
-                                               _stream_ptr(stream)))
+        fn = self._L.dctq_diag_forward_quant_planes if self._diag else self._L.dctq_forward_quant_planes
+        self._chk(fn(self._h, descs, n, C.cast(cp, C.c_void_p), C.cast(vp, C.c_void_p) if vp is not None else None,
+                     _stream_ptr(stream)))
         return outs
 
     def diag_movement_planes(self, planes, outs, stream=None, shape: int = 3, grid_mult: int = 0):
@@ -301,18 +314,23 @@ class Plan:
 
     @property
     def symbol_bytes(self) -> int:
-        """Bytes per symbol of this plan's encoder output (dctq_plan_symbol_bytes): 2 when the
-        plan bounds every |quantized coefficient| by 511, else 4."""
+        """The most compact symbol format this plan admits (dctq_plan_symbol_bytes): 2 when the
+        plan bounds every |quantized coefficient| by 511 (dctq_encode_planes16), else 4."""
         return int(self._L.dctq_plan_symbol_bytes(self._h))
 
-    def encode_planes(self, planes, outs=None, capacity=None, stream=None):
+    def encode_planes(self, planes, outs=None, capacity=None, stream=None, symbol_bytes=None):
         """Forward + zigzag/RLE of up to 4 planes (the count fused into the forward launch).
         Returns (coefs [int16 [nblk_k, 64]], offsets int32 [N+1], symbols [total]) -- offsets
-        hold uint32 bit patterns, blocks numbered plane by plane; symbols in the plan's format:
-        int32 holding (uint16)value | run << 16, or (symbol_bytes 2) int16 holding
-        run << 10 | (value & 0x3FF).  capacity (symbols) defaults to the worst case (64 per
-        block).  Reads the total back (one sync)."""
+        hold uint32 bit patterns, blocks numbered plane by plane.  symbol_bytes 4
+        (dctq_encode_planes): int32 holding (uint16)value | run << 16; 2
+        (dctq_encode_planes16, only where the plan admits it): int16 holding
+        run << 10 | (value & 0x3FF); None: the most compact format the plan admits
+        (self.symbol_bytes).  capacity (symbols) defaults to the worst case (64 per block).
+        Reads the total back (one sync)."""
         import torch
+        sb = self.symbol_bytes if symbol_bytes is None else int(symbol_bytes)
+        if sb not in (2, 4):
+            raise ValueError("symbol_bytes must be 2 or 4")
         n = len(planes)
         descs = (_Plane * n)(*[plane_desc(px) for px in planes])
         nbs = [d.nframes * (d.width // 8) * (d.height // 8) for d in descs]
@@ -323,12 +341,12 @@ class Plan:
         _need_planes(outs, None, None, nbs, planes)
         cap = 64 * nb if capacity is None else int(capacity)
         off = torch.empty(nb + 1, dtype=torch.int32, device=dev)
-        sym = torch.empty(max(cap, 1), dtype=torch.int16 if self.symbol_bytes == 2 else torch.int32, device=dev)
+        sym = torch.empty(max(cap, 1), dtype=torch.int16 if sb == 2 else torch.int32, device=dev)
         ws = torch.empty(int(self._L.dctq_encode_workspace_bytes(nb)) // 4 + 1, dtype=torch.int32, device=dev)
         cp = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
-        self._chk(self._L.dctq_encode_planes(self._h, descs, n, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
-                                        C.c_void_p(sym.data_ptr()), cap, C.c_void_p(ws.data_ptr()),
-                                        _stream_ptr(stream)))
+        fn = self._L.dctq_encode_planes16 if sb == 2 else self._L.dctq_encode_planes
+        self._chk(fn(self._h, descs, n, C.cast(cp, C.c_void_p), C.c_void_p(off.data_ptr()),
+                     C.c_void_p(sym.data_ptr()), cap, C.c_void_p(ws.data_ptr()), _stream_ptr(stream)))
         total = int(off[nb].item()) & 0xFFFFFFFF
         return outs, off, sym[:min(total, cap)]
 
@@ -354,7 +372,8 @@ class Plan:
         if out is None:
             out = torch.empty((nblk, 64), dtype=torch.float32, device=px.device)
         _need(out, nblk * 64, torch.float32, "out", px.device)
-        self._chk(self._L.dctq_forward_float(self._h, C.byref(d), C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+        fn = self._L.dctq_diag_forward_float if self._diag else self._L.dctq_forward_float
+        self._chk(fn(self._h, C.byref(d), C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
         return out
 
     def inverse(self, coef, var_num=None, out=None, stream=None):
@@ -367,9 +386,9 @@ class Plan:
         _need(out, n * 64, torch.float32, "out", coef.device)
         if var_num is not None:
             _need(var_num, n, torch.int32, "var_num", coef.device)
-        self._chk(self._L.dctq_inverse(self._h, C.c_void_p(coef.data_ptr()),
-                                  C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
-                                  n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+        fn = self._L.dctq_diag_inverse if self._diag else self._L.dctq_inverse
+        self._chk(fn(self._h, C.c_void_p(coef.data_ptr()), C.c_void_p(var_num.data_ptr()) if var_num is not None else None,
+                     n, C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
         return out
 
 

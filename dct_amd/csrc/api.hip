@@ -5,6 +5,7 @@
 // exact tie path sees bit-identical constants; the fast path's scale and guard
 // tables from the proven bound in fdct8_bound.h), validates arguments, and
 // launches the kernels of fdct8.hip / fdct8_aux.hip on the caller's stream.
+#include <dlfcn.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -43,7 +44,6 @@ int fail(int code, const char *what, hipError_t e) {
 }  // namespace dctq
 using dctq::fail;
 
-dctq::DiagKernels dctq::g_diag_kernels = {};  // filled by fdct8_diag.hip in libdct_amd_diag.so only
 
 namespace dctq {
 FastDiv make_fastdiv(uint32_t d) {
@@ -169,7 +169,7 @@ static int build_plan(const double *q, int quality, int adaptive, dctq_plan **ou
     p->adaptive = adaptive ? 1 : 0;
     p->device = dev;
     p->num_cus = prop.multiProcessorCount;
-    p->variant = 2;  // dispatch by launch size (fdct8.hip); the diagnostic library can force another
+    p->variant = 2;  // the product kernels; dctq_diag_* entry points (libdct_amd_diag.so) can force another
     p->fallbacks = nullptr;
     dctq_host::dct_matrix(8, p->host.dct);
     for (int c = 0; c < 64; ++c) {
@@ -254,34 +254,80 @@ RandIsolation::~RandIsolation() {
 }
 
 namespace {
-std::atomic<bool> g_runtime_up{false};  // some launch entry point initialised the HIP runtime
+std::atomic<bool> g_runtime_up{false};  // some entry point initialised the HIP runtime
 struct SeenKey {
     int device;
     const void *stream;
-    uint32_t entries;  // bit e: entry point e already called by this thread on (device, stream)
+    unsigned long long id;  // hipStreamGetId: a re-created stream at a reused handle has another id
+    uint32_t entries;       // bit e: entry point e already called by this thread on (device, stream)
 };
+thread_local std::vector<SeenKey> t_seen;
+constexpr unsigned long long kNoId = ~0ull;
 }  // namespace
 
+bool runtime_started() { return g_runtime_up.load(std::memory_order_acquire); }
+void note_runtime_started() { g_runtime_up.store(true, std::memory_order_release); }
+
+// The stream's identity: its handle AND its runtime id.  The HIP runtime hands a
+// destroyed stream's handle out again to the next hipStreamCreate, so the handle
+// alone would take a re-created stream's first call (the one that may create its
+// hardware queue, and reach libhsa's rand()) for a steady-state call.
+// hipStreamGetId is looked up at run time: a process may have loaded an older HIP
+// runtime than the one this library was built against (PyTorch ships its own
+// libamdhip64.so.7, without it), and a link-time reference would then keep the
+// library from loading.  Without it every stream's id reads 0 (the handle alone;
+// hosts then call dctq_stream_release before hipStreamDestroy).
+using StreamGetIdFn = hipError_t (*)(hipStream_t, unsigned long long *);
+static StreamGetIdFn stream_get_id_fn() {
+    static const StreamGetIdFn fn = (StreamGetIdFn)dlsym(RTLD_DEFAULT, "hipStreamGetId");
+    return fn;
+}
+static unsigned long long stream_id(const void *stream) {
+    const StreamGetIdFn fn = stream_get_id_fn();
+    if (!fn) return 0;
+    unsigned long long id = 0;
+    if (fn((hipStream_t)stream, &id) != hipSuccess) {  // e.g. a special handle: the handle alone
+        (void)hipGetLastError();
+        return 0;
+    }
+    return id;
+}
+
 LaunchIsolation::LaunchIsolation(const void *stream, int entry) {
-    thread_local std::vector<SeenKey> seen;
     const uint32_t bit = 1u << (entry & 31);
     int dev = -1;
-    if (g_runtime_up.load(std::memory_order_acquire) && hipGetDevice(&dev) == hipSuccess) {
-        for (SeenKey &k : seen)
-            if (k.device == dev && k.stream == stream && (k.entries & bit)) return;  // steady state: no lock
+    unsigned long long id = kNoId;
+    if (runtime_started() && hipGetDevice(&dev) == hipSuccess) {
+        id = stream_id(stream);
+        for (const SeenKey &k : t_seen)
+            if (k.device == dev && k.stream == stream && k.id == id && (k.entries & bit))
+                return;  // steady state: no lock
     }
     iso_.emplace();
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return;  // the call itself reports the error
-    g_runtime_up.store(true, std::memory_order_release);
-    for (SeenKey &k : seen)
+    note_runtime_started();
+    if (id == kNoId) id = stream_id(stream);
+    for (SeenKey &k : t_seen)
         if (k.device == dev && k.stream == stream) {
+            if (k.id != id) k = SeenKey{dev, stream, id, 0u};  // the handle now names another stream
             k.entries |= bit;
             return;
         }
     // a host that creates streams without end: forget them all now and then (each stream's
     // next first call is isolated again, which only costs that call the lock)
-    if (seen.size() >= 64) seen.clear();
-    seen.push_back(SeenKey{dev, stream, bit});
+    if (t_seen.size() >= 64) t_seen.clear();
+    t_seen.push_back(SeenKey{dev, stream, id, bit});
+}
+
+// dctq_stream_release: this thread forgets the stream (a host about to destroy it).
+void forget_stream(const void *stream) {
+    for (size_t i = 0; i < t_seen.size();)
+        if (t_seen[i].stream == stream) {
+            t_seen[i] = t_seen.back();
+            t_seen.pop_back();
+        } else {
+            ++i;
+        }
 }
 }  // namespace dctq
 
@@ -364,10 +410,13 @@ int dctq::plane_set(const dctq_plane *planes, int nplanes, int16_t *const *coef,
 
 extern "C" {
 
-// The library holds no per-stream memory since round 5 (the tie-queue kernel and its
-// pixel stash are the diagnostic library's, fdct8_diag.hip): kept for ABI compatibility.
+// The library holds no per-stream memory (the tie-queue kernel and its pixel stash
+// are the diagnostic library's, fdct8_diag.hip); the calling thread only forgets
+// the stream in its launch-isolation list, so a stream later created at the same
+// handle is isolated on its first call even where the runtime cannot tell the two
+// apart by id.
 int dctq_stream_release(void *stream) {
-    (void)stream;
+    dctq::forget_stream(stream);
     return DCTQ_OK;
 }
 
@@ -382,10 +431,6 @@ int dctq_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, i
     dctq::PlaneSet ps;
     int rc = dctq::plane_set(planes, nplanes, coef, var_num, &ps);
     if (rc) return rc;
-    if (plan->variant == 1 || plan->variant == 4) {  // diagnostic plans only (dctq_diag_plan_set_variant)
-        if (!dctq::g_diag_kernels.forward_quant) return fail(DCTQ_EINVAL, "forward variant not in this library");
-        return dctq::g_diag_kernels.forward_quant(plan, ps, (hipStream_t)stream);
-    }
     HIPCHK(dctq::launch_fdct8_quant(ps, plan->dev, plan->adaptive, plan->fallbacks, (hipStream_t)stream,
                                     plan->num_cus),
            "fdct8_quant_v3 launch");
@@ -416,14 +461,18 @@ size_t dctq_encode_workspace_bytes(long long total_blocks) {
 
 int dctq_plan_symbol_bytes(const dctq_plan *plan) { return plan ? plan->symbol_bytes : DCTQ_EINVAL; }
 
-int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
-                       uint32_t *offsets, void *symbols, long long symbols_capacity, void *workspace,
-                       void *stream) {
-    DCTQ_LAUNCH(stream, 2);
+int dctq_abi_version(void) { return DCTQ_ABI_VERSION; }
+
+static int encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                         uint32_t *offsets, void *symbols, long long symbols_capacity, void *workspace, void *stream,
+                         int symbol_bytes) {
     if (int rc = dctq::check_plan(plan)) return rc;
     if (!offsets || !workspace) return fail(DCTQ_EINVAL, "offsets/workspace is NULL");
     if (symbols_capacity < 0) return fail(DCTQ_EINVAL, "symbols_capacity < 0");
     if (((uintptr_t)symbols) % 4) return fail(DCTQ_EINVAL, "symbols must be 4-byte aligned");
+    if (symbol_bytes == 2 && plan->symbol_bytes != 2)
+        return fail(DCTQ_EINVAL, "the plan's quantized coefficients can exceed 511: 2-byte symbols cannot hold them "
+                                 "(dctq_plan_symbol_bytes == 4; use dctq_encode_planes)");
     dctq::EncodeSet es = {};
     int rc = dctq::plane_set(planes, nplanes, coef, nullptr, &es.ps);
     if (rc) return rc;
@@ -434,11 +483,25 @@ int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int npla
         if (blocks >= (1ll << 26)) return fail(DCTQ_EINVAL, "more than 2^26 - 1 blocks in one encode");
     }
     es.blk_first[nplanes] = (uint32_t)blocks;
-    HIPCHK(dctq::launch_encode(es, plan->dev, plan->adaptive, offsets, symbols, plan->symbol_bytes,
+    HIPCHK(dctq::launch_encode(es, plan->dev, plan->adaptive, offsets, symbols, symbol_bytes,
                                symbols ? (unsigned long long)symbols_capacity : 0ull, workspace, (hipStream_t)stream,
                                plan->num_cus),
            "encode launch");
     return DCTQ_OK;
+}
+
+int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                       uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
+                       void *stream) {
+    DCTQ_LAUNCH(stream, 2);
+    return encode_planes(plan, planes, nplanes, coef, offsets, symbols, symbols_capacity, workspace, stream, 4);
+}
+
+int dctq_encode_planes16(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                         uint32_t *offsets, uint16_t *symbols, long long symbols_capacity, void *workspace,
+                         void *stream) {
+    DCTQ_LAUNCH(stream, 13);
+    return encode_planes(plan, planes, nplanes, coef, offsets, symbols, symbols_capacity, workspace, stream, 2);
 }
 
 int dctq_forward_quant(const dctq_plan *plan, const dctq_plane *src, int16_t *coef, int32_t *var_num, void *stream) {
@@ -454,11 +517,8 @@ int dctq_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef
     dctq::PlaneArgs a;
     int rc = dctq::plane_args(src, &a);
     if (rc) return rc;
-    if (plan->variant == 1 && dctq::g_diag_kernels.forward_float)  // diagnostic plans only
-        HIPCHK(dctq::g_diag_kernels.forward_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
-    else
-        HIPCHK(dctq::launch_fdct8_float_pair(a, plan->dev, coef, (hipStream_t)stream, plan->num_cus),
-               "fdct8_float_pair launch");
+    HIPCHK(dctq::launch_fdct8_float_pair(a, plan->dev, coef, (hipStream_t)stream, plan->num_cus),
+           "fdct8_float_pair launch");
     return DCTQ_OK;
 }
 
@@ -471,14 +531,9 @@ int dctq_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_
     if (nblocks < 0 || nblocks >= (1ll << 40)) return fail(DCTQ_EINVAL, "bad nblocks");
     if (((uintptr_t)coef) % 16 || ((uintptr_t)recon) % 16) return fail(DCTQ_EINVAL, "coef/recon must be 16-byte aligned");
     if (nblocks == 0) return DCTQ_OK;
-    if (plan->variant == 1 && dctq::g_diag_kernels.inverse)  // diagnostic plans only
-        HIPCHK(dctq::g_diag_kernels.inverse(plan->dev, plan->adaptive, coef, var_num, nblocks, recon,
-                                            (hipStream_t)stream),
-               "idct8 launch");
-    else
-        HIPCHK(dctq::launch_idct8_pair(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream,
-                                       plan->num_cus),
-               "idct8_pair launch");
+    HIPCHK(dctq::launch_idct8_pair(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream,
+                                   plan->num_cus),
+           "idct8_pair launch");
     return DCTQ_OK;
 }
 

@@ -15,9 +15,17 @@ extern "C" {
 
 /* Force the forward kernel of a plan (test-only; libdct_amd.so picks by launch
  * size): 2 = the product dispatch, 1 = v1 (one workgroup per 256 blocks), 3 =
- * v3 (in-place ties) at any size, 4 = v2 (tie queue) at any size.  Also routes
- * dctq_forward_float / dctq_inverse to their lane-per-block kernels when 1. */
+ * v3 (in-place ties) at any size, 4 = v2 (tie queue) at any size; honoured by
+ * the dctq_diag_* entry points below (lane-per-block float / inverse when 1). */
 int dctq_diag_plan_set_variant(dctq_plan *plan, int variant);
+/* dctq_forward_quant_planes / dctq_forward_float / dctq_inverse that honour the
+ * plan's forced variant (the product entry points ignore it): variant 1 / 4 runs
+ * the retired kernel, any other plan the product entry point. */
+int dctq_diag_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                   int32_t *const *var_num, void *stream);
+int dctq_diag_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream);
+int dctq_diag_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks,
+                      float *recon, void *stream);
 
 /* The fused round trip's inverse (test-only): mode 0 forces the paired-lane fp64
  * inverse; 1 restores the plan's own choice (the fp32 inverse when the plan is

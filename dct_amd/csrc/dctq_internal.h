@@ -48,6 +48,14 @@ class LaunchIsolation {
 };
 #define DCTQ_LAUNCH(stream, entry) ::dctq::LaunchIsolation dctq_launch_isolation_((stream), (entry))
 
+// Whether some entry point has already initialised the HIP runtime in this
+// process: until then any HIP call (even hipGetDevice) may initialise it, and so
+// must be isolated.  forget_stream: the calling thread drops `stream` from its
+// launch-isolation list (dctq_stream_release).
+bool runtime_started();
+void note_runtime_started();
+void forget_stream(const void *stream);
+
 
 // Resident workgroups per CU of `kernel` at `threads` per workgroup (>= 1).  The
 // launchers cache it in a function-local static (thread-safe initialisation):
@@ -59,22 +67,17 @@ inline int resident_per_cu(K kernel, int threads) {
     return nb;
 }
 
-// Persistent grid-stride kernels launch DCTQ_GRID_MULT times their resident
+// Persistent grid-stride kernels launch kGridMult times their resident
 // workgroups; the extra ones queue and start as the first wave of workgroups
 // retires, which evens out batches of unequal cost and the launch tail
 // (profiles/r02/grid_mult_ab.log: x8 is 2.4-7 % faster than x1 on the forward,
 // round trip, inverse and encoder, outputs identical; x16/x32 regress on
-// uniform input).  The forward's stash is sized for the grid it launches.
+// uniform input).
+constexpr int kGridMult = 8;
 // Cache policy of the bulk 1 KiB output stores of every streaming kernel
 // (buffer-store aux bits, gfx950: 1 sc0, 2 nt, 16 sc1).  Non-temporal: the
 // written lines are never re-read by the kernel that writes them.
-#ifndef DCTQ_NT_AUX
-#define DCTQ_NT_AUX 2
-#endif
-
-#ifndef DCTQ_GRID_MULT
-#define DCTQ_GRID_MULT 8
-#endif
+constexpr int kNtAux = 2;
 
 // n / d and n % d by multiply-high, valid for 0 <= n < 2^31 (host-built magic).
 struct FastDiv {

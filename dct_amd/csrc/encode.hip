@@ -33,7 +33,7 @@ __device__ __forceinline__ uint32_t nz16e(uint32_t w) { return ((w & 0xFFFFu) !=
 // rounds spill at this kernel's 128-VGPR bound.
 constexpr bool kEncGroup8 = true;
 constexpr int kEncWide = 0;
-constexpr int kEncGridMult = DCTQ_GRID_MULT;  // grid multiplier of this file's streaming kernels (dctq_internal.h)
+constexpr int kEncGridMult = kGridMult;  // grid multiplier of this file's streaming kernels (dctq_internal.h)
 
 template <bool ADAPTIVE>
 __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es, const DevTables *__restrict__ dev,
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
         prefetch_batch(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fence (fdct8_core.h)
         uint32_t *off = offsets + es.blk_first[k] + (size_t)b * 64;
-        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(off));
+        asm volatile("" : "+s"(off));
         int32_t vn;
         uint32_t mlo, mhi;
         forward_flags_batch<ADAPTIVE, false>(dev, cur, stage, lane, wv, b * 64 + lane < (uint32_t)nblk, vn, mlo, mhi);
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es,
         {
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, nb * 128, 0x00020000);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(q[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
+            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(q[c], rs, lane * 16, c * 1024, kNtAux);
         }
         uint32_t run = 0;
 #pragma unroll

@@ -20,9 +20,6 @@
 // still be reading its data VGPRs; LDS returns are not ordered after that).
 #include "pair_core.h"
 
-#ifndef DCTQ_PAIR_GRID_MULT
-#define DCTQ_PAIR_GRID_MULT DCTQ_GRID_MULT  // grid multiplier of this file's streaming kernels (dctq_internal.h)
-#endif
 
 namespace dctq {
 
@@ -218,7 +215,7 @@ static hipError_t launch_persistent(K kernel, long long nblk, int num_cus, hipSt
     const int per_cu = resident_per_cu(kernel, kThreadsP);
     const long long nbatch = (nblk + 31) / 32;
     const long long want = (nbatch + kWavesP - 1) / kWavesP;
-    const long long cap = (long long)num_cus * per_cu * DCTQ_PAIR_GRID_MULT;
+    const long long cap = (long long)num_cus * per_cu * kGridMult;
     hipLaunchKernelGGL(kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(kThreadsP), 0, stream, args...);
     return hipGetLastError();
 }

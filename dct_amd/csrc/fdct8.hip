@@ -90,11 +90,11 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_quant_v3(PlaneSet ps, cons
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(out.nb * 128u), 0x00020000);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_STORE_AUX);
+        for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, kStoreAux);
         if (VAR) {
             const __amdgpu_buffer_rsrc_t rv =
                 __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(out.nb * 4u), 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, kStoreAux);
         }
     }
     if (STATS && resolved) atomicAdd(fallbacks, (unsigned long long)resolved);

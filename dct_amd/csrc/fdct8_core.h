@@ -81,11 +81,8 @@ __device__ __forceinline__ double adaptive_scale(int32_t var_num) {
 // out / m for the exact paths: every divisor of a tie-heavy plan is 1 (q >= 97 without
 // adaptation), and x / 1.0 == x exactly, so the fp64 division sequence (~11 VALU) runs
 // only when some lane of the wave has a divisor other than 1.
-#ifndef DCTQ_DIV_SKIP
-#define DCTQ_DIV_SKIP 1
-#endif
 __device__ __forceinline__ double exact_div(double out, double m) {
-    if (DCTQ_DIV_SKIP && !__builtin_amdgcn_ballot_w64(m != 1.0)) return out;
+    if (!__builtin_amdgcn_ballot_w64(m != 1.0)) return out;
     return out / m;
 }
 
@@ -95,19 +92,10 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 constexpr int kPitch2 = 136;   // bytes per block in the stage: 2-way (free) conflicts for the b32 writes
-#ifndef DCTQ_STORE_AUX
-// Cache policy of the bulk coefficient stores (gfx950: 1 sc0, 2 nt, 16 sc1).
-// Non-temporal: -15 % kernel time on the 4K stream (profiles/r01/store_policy.md);
-// the written lines are never re-read by this kernel except by tie patches,
-// which come after a vmcnt(0).
-#define DCTQ_STORE_AUX DCTQ_NT_AUX
-#endif
-#ifndef DCTQ_LOAD_NT
-#define DCTQ_LOAD_NT 1  // pixel rows are read exactly once
-#endif
-#ifndef DCTQ_ABLATE
-#define DCTQ_ABLATE 0  // diagnostic builds only (tools/ubench/ablate.sh): 1 no tie flags, 2 no butterfly, 8 flags but no queue, 16 queue without drains, 32 queue code never run, 64 no pixel loads, 128 no coefficient stores, 256 constant quant tables (no scalar table loads), 1024 no stash stores, 2048 no final drain, 4096 drains compute but do not patch, 8192 in-stage passes without the fp64 evaluation
-#endif
+// Cache policy of the bulk coefficient stores: non-temporal (kNtAux), -15 % kernel
+// time on the 4K stream (profiles/r01/store_policy.md); the written lines are never
+// re-read by this kernel except by tie patches, which come after a vmcnt(0).
+constexpr int kStoreAux = kNtAux;
 
 template <int K>
 __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
@@ -128,15 +116,6 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t w) {
 // trip (profiles/r05/forward_buf_rows_ab.log, rt_ab_keep_late_rows.log).
 template <bool BUF = true>
 __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 (&rows)[8]) {
-    if (DCTQ_ABLATE & 64) {  // diagnostic: opaque synthetic rows, no memory traffic
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            uint32_t a = n * 0x9E3779B1u + r, c = a ^ (a >> 13);
-            asm volatile("" : "+v"(a), "+v"(c));
-            rows[r] = make_uint2(a, c);
-        }
-        return;
-    }
     const uint8_t *px = block_ptr(p, n < (uint32_t)p.nblk ? n : 0);
     if constexpr (BUF) {
         if (p.span) {  // kernel argument: wave-uniform
@@ -153,12 +132,8 @@ __device__ __forceinline__ void load_rows(const PlaneArgs &p, uint32_t n, uint2 
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-#if DCTQ_LOAD_NT
         const u2v t = __builtin_nontemporal_load(reinterpret_cast<const u2v *>(px + r * p.stride));
         rows[r] = make_uint2(t.x, t.y);
-#else
-        rows[r] = *reinterpret_cast<const uint2 *>(px + r * p.stride);
-#endif
     }
 }
 
@@ -226,9 +201,8 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
     // ---- row pass, then column pairs fused with quantization
 #pragma unroll
     for (int r = 0; r < 8; ++r)
-        if (!(DCTQ_ABLATE & 2))
-            aan8(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7], DCTQ_C4, DCTQ_C6,
-                 DCTQ_C2MC6, DCTQ_C2PC6);
+        aan8(v[r][0], v[r][1], v[r][2], v[r][3], v[r][4], v[r][5], v[r][6], v[r][7], DCTQ_C4, DCTQ_C6, DCTQ_C2MC6,
+             DCTQ_C2PC6);
 
     f2 sc2 = {1.0f, 1.0f};
     if (ADAPTIVE) {
@@ -254,18 +228,16 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
 #pragma unroll
     for (int cp = 0; cp < 4; ++cp) {
         const int c0 = 2 * cp;
-        if (!(DCTQ_ABLATE & 2)) {
-            aan8(v[0][c0], v[1][c0], v[2][c0], v[3][c0], v[4][c0], v[5][c0], v[6][c0], v[7][c0], DCTQ_C4, DCTQ_C6,
-                 DCTQ_C2MC6, DCTQ_C2PC6);
-            aan8(v[0][c0 + 1], v[1][c0 + 1], v[2][c0 + 1], v[3][c0 + 1], v[4][c0 + 1], v[5][c0 + 1], v[6][c0 + 1],
-                 v[7][c0 + 1], DCTQ_C4, DCTQ_C6, DCTQ_C2MC6, DCTQ_C2PC6);
-        }
+        aan8(v[0][c0], v[1][c0], v[2][c0], v[3][c0], v[4][c0], v[5][c0], v[6][c0], v[7][c0], DCTQ_C4, DCTQ_C6,
+             DCTQ_C2MC6, DCTQ_C2PC6);
+        aan8(v[0][c0 + 1], v[1][c0 + 1], v[2][c0 + 1], v[3][c0 + 1], v[4][c0 + 1], v[5][c0 + 1], v[6][c0 + 1],
+             v[7][c0 + 1], DCTQ_C4, DCTQ_C6, DCTQ_C2MC6, DCTQ_C2PC6);
         if (cp == 0) v[0][0] -= 8192.0f;  // 64 * 128: exact (integer < 2^24)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const int c = i * 8 + c0, slot = 16 * cp + 2 * i;
             const f2 y = {v[i][c0], v[i][c0 + 1]};
-            f2 w = (DCTQ_ABLATE & 256) ? f2{0.0625f + slot * 1e-3f, 0.0625f} : f2{tp->ws[slot], tp->ws[slot + 1]};
+            f2 w = {tp->ws[slot], tp->ws[slot + 1]};
             if (ADAPTIVE) {
                 if (c == 0) w.y *= sc2.y;  // the DC keeps Q (src/quantization.c:198-199)
                 else w *= sc2;
@@ -273,10 +245,9 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
             const f2 tt = __builtin_elementwise_fma(y, w, M2);
             const f2 nr = M2 - tt;
             const f2 f = __builtin_elementwise_fma(y, w, nr);
-            const f2 T = (DCTQ_ABLATE & 256) ? f2{0.25f, 0.25f} : f2{tp->t2s[slot], tp->t2s[slot + 1]};
+            const f2 T = {tp->t2s[slot], tp->t2s[slot + 1]};
             const f2 d = __builtin_elementwise_fma(-f, f, T);  // < 0  <=>  |f| beyond the guard
-            if (DCTQ_ABLATE & 1) {
-            } else if (cp < 2) {
+            if (cp < 2) {
                 mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.x), 31);
                 mlo = __builtin_amdgcn_alignbit(mlo, __float_as_uint(d.y), 31);
             } else {
@@ -298,7 +269,7 @@ __device__ __forceinline__ void fdct8_compute(const DevTables *__restrict__ dev,
 // DC (processing slot 0 = bit 31 of mlo) is flagged.
 __device__ __forceinline__ void flat_dc_fix(const DevTables *__restrict__ dev, const uint2 (&cur)[8], uint4 *stage,
                                             int lane, int wv, uint32_t &mlo) {
-    if (!(DCTQ_ABLATE & 8) && __builtin_amdgcn_ballot_w64((mlo >> 31) != 0u)) {
+    if (__builtin_amdgcn_ballot_w64((mlo >> 31) != 0u)) {
         const uint32_t w = cur[0].x;
         bool flat = w == (w & 0xFFu) * 0x01010101u;
 #pragma unroll
@@ -311,21 +282,18 @@ __device__ __forceinline__ void flat_dc_fix(const DevTables *__restrict__ dev, c
 }
 
 // temp[k][j] = sum_l x[k][l] D^T[l][j], l ascending from 0.0 (src/dct.c:57-64), x = px - 128.
-// DCTQ_EXACT_NOZERO starts the sum at the first product instead of 0.0 + it (and
-// the callers start `out` at its first term): 0.0 + p == p for every p except
-// p == -0.0, so the sums differ at most in the sign of a zero, which neither a
-// later nonzero term nor round() / the int conversion can see -- the int16
-// result is the reference's.  9 fp64 adds fewer per evaluation.
-#ifndef DCTQ_EXACT_NOZERO
-#define DCTQ_EXACT_NOZERO 1
-#endif
+// The sum starts at the first product instead of 0.0 + it (and the callers start
+// `out` at its first term): 0.0 + p == p for every p except p == -0.0, so the sums
+// differ at most in the sign of a zero, which neither a later nonzero term nor
+// round() / the int conversion can see -- the int16 result is the reference's
+// (DESIGN.md 4).  9 fp64 adds fewer per evaluation.
 __device__ __forceinline__ double row_sum(uint32_t wx, uint32_t wy, const double *dj) {
     double t = 0.0;
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
         const uint32_t w = l < 4 ? wx : wy;
         const double p = ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * dj[l];
-        t = l == 0 && DCTQ_EXACT_NOZERO ? p : t + p;
+        t = l == 0 ? p : t + p;
     }
     return t;
 }
@@ -364,7 +332,7 @@ __device__ __forceinline__ int exact_from_rows(const uint2 (&rows)[8], int c, co
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const double t = row_sum(rows[k].x, rows[k].y, dj);
-        out = k == 0 && DCTQ_EXACT_NOZERO ? di[0] * t : out + di[k] * t;
+        out = k == 0 ? di[0] * t : out + di[k] * t;
     }
     return (int)round(exact_div(out, m));
 }
@@ -451,7 +419,7 @@ __device__ __forceinline__ int exact_from_rows_lds(const uint2 (&rows)[8], int c
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const double t = row_sum(rows[k].x, rows[k].y, dj);
-        out = k == 0 && DCTQ_EXACT_NOZERO ? di[0] * t : out + di[k] * t;
+        out = k == 0 ? di[0] * t : out + di[k] * t;
     }
     return (int)round(exact_div(out, m));
 }
@@ -493,7 +461,7 @@ __device__ __forceinline__ void group_sum(const double (&t)[8 / G], const double
             tq = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
         }
         const double p = di[Q] * tq;
-        out = Q == 0 && DCTQ_EXACT_NOZERO ? p : out + p;
+        out = Q == 0 ? p : out + p;
         group_sum<G, Q + 1>(t, di, out);
     }
 }
@@ -529,7 +497,7 @@ __device__ __forceinline__ uint32_t exact_grouped(const ExactTables *tab, const 
             for (int i = 0; i < R; ++i) {
                 const uint32_t w = l < 4 ? rx[i] : ry[i];
                 const double p = ((double)((w >> (8 * (l & 3))) & 0xFFu) - 128.0) * d;
-                t[i] = l == 0 && DCTQ_EXACT_NOZERO ? p : (l == 0 ? 0.0 + p : t[i] + p);
+                t[i] = l == 0 ? p : t[i] + p;
             }
         }
     }
@@ -573,7 +541,7 @@ __device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict_
                                                     uint32_t &mlo, uint32_t &mhi) {
     fdct8_compute<ADAPTIVE, VAR>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
     flat_dc_fix(dev, cur, stage, lane, wv, mlo);
-    if (!valid || (DCTQ_ABLATE & 8)) mlo = mhi = 0;
+    if (!valid) mlo = mhi = 0;
 }
 
 // Phase 2 (after the prefetch fence): the batch's flagged coefficients resolved
@@ -585,9 +553,7 @@ __device__ __forceinline__ void forward_flags_batch(const DevTables *__restrict_
 // value (tables in LDS) and writes it into the stage.  `scr` = 64 uint16 of the
 // wave's LDS (entry = coefficient | block lane << 6).  Call after the prefetch
 // fence.  Returns the entries this lane resolved.
-#ifndef DCTQ_GROUP8_MAX
-#define DCTQ_GROUP8_MAX 8u  // GROUP8 passes with up to this many entries run in rounds of 8 lanes per entry
-#endif
+constexpr uint32_t kGroup8Max = 8u;  // GROUP8 passes with up to this many entries run in rounds of 8 lanes per entry
 // WIDE (with GROUP8): bit 0 / bit 1 -- passes of 9..16 / 17..32 entries run as one round of
 // 4 / 2 lanes per entry (exact_grouped) instead of one entry per lane.  Per kernel: the
 // register-bound kernels (128 VGPRs at 4 waves/SIMD) spill with them.
@@ -612,7 +578,7 @@ __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab,
         }
         wave_sync();
         if constexpr (GROUP8) {
-            if (e <= DCTQ_GROUP8_MAX) {  // wave-uniform: rounds of 8 entries (~100 VALU each, against ~290 for a pass)
+            if (e <= kGroup8Max) {  // wave-uniform: rounds of 8 entries (~100 VALU each, against ~290 for a pass)
                 for (uint32_t e0 = 0; e0 < e; e0 += 8u)
                     mine += exact_grouped<8, ADAPTIVE>(tab, cur, st16, scr + e0, lane, e - e0 < 8u ? e - e0 : 8u);
                 wave_sync();
@@ -639,10 +605,7 @@ __device__ __forceinline__ uint32_t resolve_ties_compact(const ExactTables *tab,
         }
         if ((uint32_t)lane < e) {
             const int c = (int)(ent & 63u);
-            if (DCTQ_ABLATE & 8192)  // diagnostic: entries compacted and rows pulled, no fp64 evaluation
-                st16[src * (kPitch2 / 2) + c] = (int16_t)(rows[0].x ^ rows[3].y ^ rows[7].x ^ (uint32_t)c);
-            else
-                st16[src * (kPitch2 / 2) + c] = (int16_t)exact_from_rows_lds<ADAPTIVE>(rows, c, tab);
+            st16[src * (kPitch2 / 2) + c] = (int16_t)exact_from_rows_lds<ADAPTIVE>(rows, c, tab);
             ++mine;
         }
         wave_sync();  // the next pass rewrites scr
@@ -664,13 +627,10 @@ __device__ __forceinline__ void stage_chunks(const uint4 *stage, int wv, int lan
 }
 
 // A batch's coefficient destination (plane k's output + its 64-block batch b, and the
-// blocks it holds), resolved where it is called.  DCTQ_PIN_OUT pins the values in
+// blocks it holds), resolved where it is called.  pin_sgpr pins the values in
 // SGPRs there: without it LLVM re-issues their kernel-argument loads after the
 // prefetch fence (an asm with a "memory" clobber), so a scalar-cache round trip sits
 // between the rows' arrival and the stores of every batch.
-#ifndef DCTQ_PIN_OUT
-#define DCTQ_PIN_OUT 1
-#endif
 struct BatchOut {
     char *base;   // output of block 0 of the batch
     int32_t *var; // var_num of block 0 of the batch (if the plane set has var_num outputs)
@@ -682,7 +642,7 @@ __device__ __forceinline__ BatchOut batch_out(const PlaneSet &ps, int k, uint32_
     o.nb = left < 64u ? left : 64u;
     o.base = reinterpret_cast<char *>(ps.coef[k]) + (size_t)b * 64 * 128;
     o.var = ps.var[k] ? ps.var[k] + (size_t)b * 64 : nullptr;
-    if (DCTQ_PIN_OUT) asm volatile("" : "+s"(o.nb), "+s"(o.base), "+s"(o.var));
+    asm volatile("" : "+s"(o.nb), "+s"(o.base), "+s"(o.var));
     return o;
 }
 
@@ -694,12 +654,9 @@ __device__ __forceinline__ void retire_stores() { __builtin_amdgcn_s_waitcnt(0x0
 // wave pays that tail once (forward -0.3 to -7 %, q100 most; the fused round trip
 // measured +1 % and keeps the load of the last plane's block 0:
 // profiles/r02/grid_mult_ab.log).
-#ifndef DCTQ_SKIP_TAIL_PF
-#define DCTQ_SKIP_TAIL_PF 1
-#endif
 template <bool SKIP = true, bool BUF = true>
 __device__ __forceinline__ void prefetch_batch(const PlaneSet &ps, uint32_t gn, int lane, uint2 (&nxt)[8]) {
-    if (SKIP && DCTQ_SKIP_TAIL_PF && gn >= ps.first[ps.n]) return;  // wave-uniform
+    if (SKIP && gn >= ps.first[ps.n]) return;  // wave-uniform
     const int kn = plane_of(ps, gn);
     load_rows<BUF>(ps.pl[kn], (gn - first_of(ps, kn)) * 64 + lane, nxt);
 }

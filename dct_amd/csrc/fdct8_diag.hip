@@ -11,7 +11,8 @@
 //     f64_pair.hip);
 //   * the no-arithmetic movement twins of the forward and round-trip kernels
 //     (bench.py's same-box ceilings).
-// The product's entry points reach the variants through dctq::g_diag_kernels,
+// The diagnostic entry points dctq_diag_forward_quant_planes / _forward_float / _inverse
+// reach the variants (the product entry points never do),
 // which this file fills when the diagnostic library loads.
 #include <map>
 #include <mutex>
@@ -24,6 +25,14 @@
 #include "pair_core.h"
 #include "plan.h"
 
+// Timing ablations of the retired kernels here (diagnostic builds only, -DDCTQ_ABLATE=m):
+// 1 no tie flags, 8 flags but no queue, 16 queue without drains, 32 queue code never
+// run, 128 no coefficient stores, 1024 no stash stores, 2048 no final drain, 4096
+// drains compute but do not patch.  0 in every build this tree makes.
+#ifndef DCTQ_ABLATE
+#define DCTQ_ABLATE 0
+#endif
+
 namespace dctq {
 
 // ---- the v2 queue kernel's constants
@@ -35,7 +44,7 @@ static_assert(kQCap <= 128, "queue entries hold the stash slot in 7 bits");
 #ifndef DCTQ_STASH_DEDUP
 #define DCTQ_STASH_DEDUP 1  // one pixel stash per flagged block and batch (its entries share it)
 #endif
-constexpr int kV2GridMult = DCTQ_GRID_MULT;  // fdct8_quant_v2's grid (its stash is sized to it: 8 KiB per wave)
+constexpr int kV2GridMult = kGridMult;  // fdct8_quant_v2's grid (its stash is sized to it: 8 KiB per wave)
 
 // Where the v2 forward gets its tie-path pixel stash: get(ctx, bytes) returns
 // device memory of at least `bytes` that no other in-flight launch uses, or
@@ -387,12 +396,12 @@ __device__ __forceinline__ void fdct8_batch(const PlaneSet &ps, const DevTables 
             for (int k = 0; k < 8; ++k) asm volatile("" ::"v"(val[k]));
         } else {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_STORE_AUX);
+            for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, kStoreAux);
         }
         if (VAR) {
             const __amdgpu_buffer_rsrc_t rv =
                 __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(out.nb * 4u), 0x00020000);
-            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, kStoreAux);
         }
     }
 
@@ -588,7 +597,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement(PlaneSet ps, cons
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(out.nb * 128u), 0x00020000);
 #pragma unroll
-        for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_STORE_AUX);
+        for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, kStoreAux);
     }
 }
 
@@ -632,7 +641,7 @@ __global__ __launch_bounds__(kFThreads, 4) void fdct8_movement_v2(PlaneSet ps) {
         u4v val[8];
         stage_chunks(stage, wv, lane, val);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) __builtin_amdgcn_raw_buffer_store_b128(val[q], rs, lane * 16, q * 1024, DCTQ_STORE_AUX);
+        for (int q = 0; q < 8; ++q) __builtin_amdgcn_raw_buffer_store_b128(val[q], rs, lane * 16, q * 1024, kStoreAux);
     }
 }
 
@@ -797,7 +806,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip_movement(RoundTrip
         prefetch_batch<false>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
-        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
+        asm volatile("" : "+s"(recon));
         uint2 *mine2 = reinterpret_cast<uint2 *>(wstage + lane * kPitch2);
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
@@ -813,7 +822,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip_movement(RoundTrip
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
+            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, kNtAux);
         }
         char *mine = wstage + j * kPitchP + h * 128;
 #pragma unroll
@@ -980,11 +989,49 @@ int diag_forward_quant(const dctq_plan *plan, const dctq::PlaneSet &ps, hipStrea
     return DCTQ_OK;
 }
 
-struct RegisterDiagKernels {
-    RegisterDiagKernels() {
-        dctq::g_diag_kernels.forward_quant = diag_forward_quant;
-        dctq::g_diag_kernels.forward_float = dctq::launch_fdct8_float;
-        dctq::g_diag_kernels.inverse = dctq::launch_idct8;
-    }
-} g_register_diag_kernels;
 }  // namespace
+
+extern "C" {
+
+// The diagnostic library's own forward / float / inverse entry points: a plan's
+// forced variant (dctq_diag_plan_set_variant) picks the retired kernel here, any
+// other plan runs the product entry point.  The product entry points never look at
+// the variant.
+int dctq_diag_forward_quant_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                                   int32_t *const *var_num, void *stream) {
+    if (!plan || (plan->variant != 1 && plan->variant != 4))
+        return dctq_forward_quant_planes(plan, planes, nplanes, coef, var_num, stream);
+    if (int rc = dctq::check_plan(plan)) return rc;
+    dctq::PlaneSet ps;
+    if (int rc = dctq::plane_set(planes, nplanes, coef, var_num, &ps)) return rc;
+    return diag_forward_quant(plan, ps, (hipStream_t)stream);
+}
+
+int dctq_diag_forward_float(const dctq_plan *plan, const dctq_plane *src, float *coef, void *stream) {
+    if (!plan || plan->variant != 1) return dctq_forward_float(plan, src, coef, stream);
+    DCTQ_LAUNCH(stream, 3);
+    if (int rc = dctq::check_plan(plan)) return rc;
+    if (!coef || ((uintptr_t)coef) % 16) return dctq::fail(DCTQ_EINVAL, "coef NULL or not 16-byte aligned");
+    dctq::PlaneArgs a;
+    if (int rc = dctq::plane_args(src, &a)) return rc;
+    HIPCHK(dctq::launch_fdct8_float(a, plan->dev, coef, (hipStream_t)stream), "fdct8_float launch");
+    return DCTQ_OK;
+}
+
+int dctq_diag_inverse(const dctq_plan *plan, const int16_t *coef, const int32_t *var_num, long long nblocks,
+                      float *recon, void *stream) {
+    if (!plan || plan->variant != 1) return dctq_inverse(plan, coef, var_num, nblocks, recon, stream);
+    DCTQ_LAUNCH(stream, 4);
+    if (int rc = dctq::check_plan(plan)) return rc;
+    if (!coef || !recon) return dctq::fail(DCTQ_EINVAL, "coef/recon is NULL");
+    if (plan->adaptive && !var_num) return dctq::fail(DCTQ_EINVAL, "adaptive inverse needs var_num");
+    if (nblocks < 0 || nblocks >= (1ll << 40)) return dctq::fail(DCTQ_EINVAL, "bad nblocks");
+    if (((uintptr_t)coef) % 16 || ((uintptr_t)recon) % 16)
+        return dctq::fail(DCTQ_EINVAL, "coef/recon must be 16-byte aligned");
+    if (nblocks == 0) return DCTQ_OK;
+    HIPCHK(dctq::launch_idct8(plan->dev, plan->adaptive, coef, var_num, nblocks, recon, (hipStream_t)stream),
+           "idct8 launch");
+    return DCTQ_OK;
+}
+
+}  // extern "C"

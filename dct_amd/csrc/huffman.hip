@@ -38,18 +38,11 @@
 // compacted through LDS -- add one count per run length into the same shared
 // region (Hist), and run the bucket merge there.  VALU- and LDS-latency-bound
 // at 3 waves/SIMD.
-// DCTQ_HUF_MIN_WAVES (launch bound, default 3 waves/SIMD: 168 VGPRs) is an A/B knob.
 #include <type_traits>
 
 #include "dctq_internal.h"
 #include "fdct8_core.h"
 
-#ifndef DCTQ_HUF_ABLATE
-#define DCTQ_HUF_ABLATE 0  // timing ablations of the narrow path (tools/huf_ab.py libvar_no*): 1 no leaves/merge, 2 no merge (clear only), 3 leaves + read-back, no merge
-#endif
-#ifndef DCTQ_HUF_DMA_POLICY
-#define DCTQ_HUF_DMA_POLICY "nt"  // cache policy of the tile DMA (read once)
-#endif
 
 namespace dctq {
 
@@ -239,7 +232,7 @@ __device__ __forceinline__ void tile_dma(const int16_t *coef, long long t, long 
         asm volatile(
             "s_mov_b32 %0, m0\n\t"
             "s_mov_b32 m0, %1\n\t"
-            "buffer_load_dwordx4 %2, %3, 0 offen " DCTQ_HUF_DMA_POLICY " lds\n\t"
+            "buffer_load_dwordx4 %2, %3, 0 offen nt lds\n\t"  // non-temporal: the tile is read once
             "s_mov_b32 m0, %0"
             : "=&s"(save)
             : "s"(lds + c * 1024), "v"(c * 1024 + (base ^ ((c & 1) << 6))), "s"(rs)
@@ -340,10 +333,7 @@ __device__ __forceinline__ void dense_runs(char *mine, const Hist &h, int lane, 
 // and runs the register merge).  A software-pipelined kernel loop that merged one
 // tile while the next tile's LDS phases were in flight measured no faster
 // (profiles/r03/huffman_restructure_ab.log).
-#ifndef DCTQ_HUF_HEAVY_ROWS
-#define DCTQ_HUF_HEAVY_ROWS 4
-#endif
-constexpr int kHeavyRows = DCTQ_HUF_HEAVY_ROWS;  // weight rows 17.. read back without waiting (q50 noise: largest leaf ~20)
+constexpr int kHeavyRows = 4;  // weight rows 17.. read back without waiting (q50 noise: largest leaf ~20)
 struct NarrowLeaves {
     uint32_t light[16];  // weight rows 1..16 as read (the wave's byte at 8 * wave)
     uint32_t heavy[kHeavyRows];  // weight rows 17..16 + kHeavyRows as read, when hrows > 16
@@ -402,13 +392,6 @@ __device__ __forceinline__ void narrow_leaves(const char *mine, char *ctr, int l
             for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) raw[s_] = take_raw((uint32_t)s_);
         }
     }
-#if DCTQ_HUF_ABLATE == 1  // timing: count + readout only
-    L.light[0] = raw[0] + raw[7];
-    L.hrows = 16;
-    L.hn = L.hs = L.hmx = 0;
-    L.hmn = 0xFFu;
-    return;
-#endif
     // A counter is kept as its leaf's address: one v_perm moves the wave's byte of
     // the returned dword into byte 1 (the row) over the lane's byte 0 -- no extract
     // -- and the largest address gives the largest leaf weight.
@@ -428,16 +411,6 @@ __device__ __forceinline__ void narrow_leaves(const char *mine, char *ctr, int l
     }
     const uint32_t lmax = amax >> 8;  // the largest leaf weight
     (void)take_raw(0);  // row 0: the empties
-#if DCTQ_HUF_ABLATE == 2  // timing: leaf adds, then a plain clear instead of the read-back
-    uint32_t acc = 0;
-#pragma unroll
-    for (int s_ = 1; s_ < 65; ++s_) acc += take_raw((uint32_t)s_);
-    L.light[0] = acc;
-    L.hrows = 16;
-    L.hn = L.hs = L.hmx = 0;
-    L.hmn = 0xFFu;
-    return;
-#endif
     // weight rows 1..16 issued together (independent reads, all in flight; their
     // results are used by narrow_merge), each row cleared
 #pragma unroll
@@ -475,9 +448,6 @@ __device__ __forceinline__ void narrow_leaves(const char *mine, char *ctr, int l
 // Returns the WPL.
 __device__ __forceinline__ uint32_t narrow_merge(const NarrowLeaves &L, int wv) {
     const uint32_t sh = 8u * (uint32_t)wv;
-#if DCTQ_HUF_ABLATE == 1 || DCTQ_HUF_ABLATE == 2
-    return L.light[0] >> sh;
-#endif
     uint32_t cnt[17];
 #pragma unroll
     for (int w = 1; w <= 16; ++w) cnt[w] = (L.light[w - 1] >> sh) & 0xFFu;
@@ -497,12 +467,6 @@ __device__ __forceinline__ uint32_t narrow_merge(const NarrowLeaves &L, int wv) 
     hs += L.hs;
     hmn = min(hmn, L.hmn);
     hmx = max(hmx, L.hmx);
-#if DCTQ_HUF_ABLATE == 3  // timing: leaves and read-back, no merge
-    uint32_t s3 = hn + hs;
-#pragma unroll
-    for (int w = 1; w <= 16; ++w) s3 += cnt[w];
-    return s3;
-#endif
     // p: the pending node's weight (0: none); pm: pending-merge nodes (bit = weight);
     // qp: pairs of w = 9..16 (weight 2w > 16, at most 3 per w because node weights
     // add up to <= 65) as 2-bit fields at 2 (w - 9), qs: their weights.
@@ -580,11 +544,9 @@ __device__ __forceinline__ uint32_t narrow_merge(const NarrowLeaves &L, int wv) 
     return acc + hs + fin - L.count;
 }
 
-#ifndef DCTQ_HUF_BITS_AUX
 // Non-temporal bits stores (written once, never re-read here): -1.6 to -2.9 % on every input, three
 // passes on one box (profiles/r02/huffman_dma_ab.log).
-#define DCTQ_HUF_BITS_AUX 2
-#endif
+constexpr int kHufBitsAux = kNtAux;
 // A tile's classification (tile_row layout, blocks past the end zeroed).
 struct TileClass {
     uint32_t nz;        // the lane's nonzero count (exact unless narrow: then 0, unused)
@@ -674,11 +636,7 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int la
     uint32_t nodes = last_zero ? 1u : 0u;
     uint32_t lmax = last_zero ? 1u : 0u;  // the largest leaf weight (dense paths)
     const bool dense = __builtin_amdgcn_ballot_w64(nz > 32) != 0;
-#ifdef DCTQ_HUF_UNIFORM_MERGE
-    const bool lane_merge = false;
-#else
     const bool lane_merge = dense;  // the dense paths merge per lane (occupancy mask)
-#endif
     uint32_t wpl = 0, pending = 0;
     if (!__builtin_amdgcn_ballot_w64(nz > 16))
         sparse_runs<16, FWD>(mine, h, lane, nodes, lmax, next_tile);
@@ -773,10 +731,6 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int la
 template <bool FWD = false, typename NextTile>
 __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, int wv, int nb, NextTile next_tile) {
     const TileClass cl = classify<FWD>(mine, lane, nb);
-#ifdef DCTQ_HUF_ABLATE_FLOOR  // timing ablation only: the tile load and classification, no sizes
-    next_tile();
-    return cl.nz + cl.span;
-#endif
     if (cl.narrow) {
         NarrowLeaves L;
         narrow_leaves<FWD>(mine, ctr, lane, wv, cl.vmin, cl.span, cl.last_zero, next_tile, L);  // the zero leaf included
@@ -785,19 +739,19 @@ __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, i
     return sort_tile_bits<FWD>(mine, ctr, lane, wv, nb, cl, next_tile);
 }
 
-#ifndef DCTQ_HP_GROUP8
-#define DCTQ_HP_GROUP8 1  // passes of <= 8 entries run 8 lanes per entry (exact_grouped<8>): -4.1 % uniform, -3.1 % smooth
-#endif
-#ifndef DCTQ_HP_WIDE
-// passes of 9..32 entries in one round of 4 / 2 lanes per entry (resolve_ties_compact WIDE):
-// -2.7 % on extreme q10 (~10 entries per batch), uniform q50 unchanged (profiles/r04/wide_groups_ab.log);
-// no scratch at this kernel's 168-VGPR bound
-#define DCTQ_HP_WIDE 3
-#endif
-#ifndef DCTQ_HUF_MIN_WAVES
-#define DCTQ_HUF_MIN_WAVES 3
-#endif
-__global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
+// The tie passes of huffman_from_pixels: passes of <= 8 entries run 8 lanes per entry
+// (exact_grouped<8>): -4.1 % uniform, -3.1 % smooth; passes of 9..32 entries in one round of
+// 4 / 2 lanes per entry (resolve_ties_compact WIDE = 3): -2.7 % on extreme q10 (~10 entries per
+// batch), uniform q50 unchanged (profiles/r04/wide_groups_ab.log); no scratch at this kernel's
+// 168-VGPR bound.
+constexpr bool kHpGroup8 = true;
+constexpr int kHpWide = 3;
+// Launch bound of both kernels: 3 waves/SIMD (168 VGPRs; 4 spilled, profiles/r01).
+constexpr int kHufMinWaves = 3;
+// Workgroups per CU in the grid: 3 are resident (LDS-bound) and the rest queue behind them, so
+// tiles of unequal cost balance (8: +1-2.5 %, 3: +3-4 %).
+constexpr long long kHufGridPerCu = 16;
+__global__ __launch_bounds__(kHufThreads, kHufMinWaves) void huffman_bits_kernel(const int16_t *__restrict__ coef, long long nblk,
                                                                    uint32_t *__restrict__ bits, long long ntiles) {
     // per wave: the tile stage (9 KiB), reused for the sparse keys; per workgroup: the counters and histograms
     __shared__ uint4 lds[kHufWaves * kHufWaveLds / 16];
@@ -812,7 +766,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
     long long t = (long long)blockIdx.x * kHufWaves + wv;
     auto store_bits = [&](uint32_t out, long long tt, int n) {
         const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(bits + tt * 64, (short)0, n * 4, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
+        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, kHufBitsAux);
     };
     if (t < ntiles) tile_dma(coef, t, nblk, mine, lane);
     for (; t < ntiles; t += stride) {
@@ -840,16 +794,10 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_bits_
 hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bits, hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
     long long grid = (ntiles + kHufWaves - 1) / kHufWaves;
-#ifndef DCTQ_HUF_GRID_PER_CU
-#define DCTQ_HUF_GRID_PER_CU 16  // workgroups per CU in the grid: 3 are resident (LDS-bound) and the rest queue behind them, so tiles of unequal cost balance (8: +1-2.5 %, 3: +3-4 %)
-#endif
-    const long long cap = (long long)num_cus * DCTQ_HUF_GRID_PER_CU;
+    const long long cap = (long long)num_cus * kHufGridPerCu;
     if (grid > cap) grid = cap;
-#ifndef DCTQ_HUF_LDS_PAD
-#define DCTQ_HUF_LDS_PAD 0  // A/B: dynamic LDS padding, fewer workgroups per CU (occupancy sensitivity)
-#endif
-    hipLaunchKernelGGL(huffman_bits_kernel, dim3((unsigned)grid), dim3(kHufThreads), DCTQ_HUF_LDS_PAD, stream, coef,
-                       nblk, bits, ntiles);
+    hipLaunchKernelGGL(huffman_bits_kernel, dim3((unsigned)grid), dim3(kHufThreads), 0, stream, coef, nblk, bits,
+                       ntiles);
     return hipGetLastError();
 }
 
@@ -865,7 +813,7 @@ hipError_t launch_huffman_bits(const int16_t *coef, long long nblk, uint32_t *bi
 // as soon as the tie pass is done with them, so the loads fly through the size
 // computation (-3.4 %).
 template <bool ADAPTIVE>
-__global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_pixels_kernel(EncodeSet es,
+__global__ __launch_bounds__(kHufThreads, kHufMinWaves) void huffman_from_pixels_kernel(EncodeSet es,
                                                                                               const DevTables *__restrict__ dev,
                                                                                               uint32_t *__restrict__ bits) {
     __shared__ uint4 lds[kHufWaves * kHufWaveLds / 16];
@@ -902,11 +850,8 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         fdct8_compute<ADAPTIVE, false>(dev, cur, stage, lane, wv, mlo, mhi, var_num);
         flat_dc_fix(dev, cur, stage, lane, wv, mlo);
         if (!valid) mlo = mhi = 0;
-#ifdef DCTQ_HP_ABLATE_TIES  // timing ablation only: flagged coefficients keep their fast-path value
-        mlo = mhi = 0;
-#endif
         if (__builtin_amdgcn_ballot_w64((mlo | mhi) != 0))
-            (void)resolve_ties_compact<ADAPTIVE, DCTQ_HP_GROUP8, DCTQ_HP_WIDE>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
+            (void)resolve_ties_compact<ADAPTIVE, kHpGroup8, kHpWide>(&tab, cur, stage, scr, lane, wv, mlo, mhi);
         wave_sync();
         prefetch_batch<true, false>(ps, g + step, lane, cur);  // the rows are dead now; nothing past the last batch
         if (nb < 64) {  // blocks past the end are empty
@@ -921,7 +866,7 @@ __global__ __launch_bounds__(kHufThreads, DCTQ_HUF_MIN_WAVES) void huffman_from_
         // (pinning this destination in SGPRs at the top, as the forward kernels do, spilled 8 B here)
         const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
             bits + es.blk_first[k] + (size_t)b * 64, (short)0, nb * 4, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, DCTQ_HUF_BITS_AUX);
+        __builtin_amdgcn_raw_buffer_store_b32(out, rb, lane * 4, 0, kHufBitsAux);
         // tile_bits leaves the stage to the next batch's forward only after its own reads
         __builtin_amdgcn_s_waitcnt(0xC07F);
         wave_sync();
@@ -932,7 +877,7 @@ hipError_t launch_huffman_from_pixels(const EncodeSet &es, const DevTables *dev,
                                       hipStream_t stream, int num_cus) {
     const uint32_t nbatch = es.ps.first[es.ps.n];
     long long grid = ((long long)nbatch + kHufWaves - 1) / kHufWaves;
-    const long long cap = (long long)num_cus * DCTQ_HUF_GRID_PER_CU;  // a persistent grid (3 per CU) is +11 %
+    const long long cap = (long long)num_cus * kHufGridPerCu;  // a persistent grid (3 per CU) is +11 %
     if (grid > cap) grid = cap;
     if (grid < 1) return hipSuccess;
     if (adaptive)

@@ -17,6 +17,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <optional>
 #include <vector>
 
 #include "dct.h"
@@ -149,59 +151,108 @@ __global__ void k_variance(int nn, const double *__restrict__ x, double *__restr
     out[0] = (s2 / nn) - (mean * mean);
 }
 
-// ---------------------------------------------------------------- staging
-// Zero-copy: one pinned, device-mapped host buffer.  A call packs its row-pointer
-// arrays into it, launches a kernel that reads its inputs from it and writes its
-// outputs back into it over the host link, and synchronizes: no memcpy calls.
-// Larger blocks go through a device scratch buffer instead (copied once each
-// way).  One buffer of each per device (the current one at the call: a host may
-// switch devices between calls): every entry point holds the library-wide entry
-// lock (DCTQ_ENTRY), so calls never overlap, and a thread that exits leaves
-// nothing behind.  Both are grown on demand and kept for the life of the
-// process (their memory goes back with it).
-struct Staging {
+// ---------------------------------------------------------------- lanes
+// The reference API is reentrant and keeps no mutable global state (its only
+// static, src/quantization.c:8, is const; SURVEY 8(b) ran 8 pthreads over one
+// context), so calls from different host threads must overlap here too.  Each
+// thread gets one LANE per device: its own non-blocking stream, a pinned,
+// device-mapped staging buffer (zero-copy: a call packs its row-pointer arrays
+// into it, the kernel reads its inputs from it and writes its outputs back into
+// it over the host link, and the call synchronizes its own stream -- no memcpy
+// calls) and, for large blocks, a device scratch buffer.  No lock is held in
+// steady state: only a thread's FIRST call on a device (it creates the lane's
+// stream and launches on it first, which is where libhsa may call srand/rand)
+// and a buffer's growth (a HIP allocation) take the rand isolation lock
+// (dctq_internal.h), like the batched entry points' first calls.
+//
+// Lanes are never freed: a thread that exits hands its lanes to a pool (no HIP
+// call runs in a thread-exit destructor) and the next thread that needs a lane
+// on that device takes it, so a host that keeps spawning threads holds at most
+// as many lanes as it ever had threads alive at once.
+constexpr size_t kStageMin = 64 * 1024;  // every n <= 32 call fits without growing
+struct Lane {
+    int device = -1;
+    hipStream_t stream = nullptr;
     unsigned char *host = nullptr;  // pinned host memory
-    unsigned char *dev = nullptr;   // the same pages as seen by the device
-    size_t bytes = 0;
-    unsigned char *get(size_t need) {
-        if (need > bytes) {
+    unsigned char *hdev = nullptr;  // the same pages as seen by the device
+    size_t host_bytes = 0;
+    unsigned char *scratch = nullptr;
+    size_t scratch_bytes = 0;
+    unsigned char *stage(size_t need) {
+        if (need > host_bytes) {
+            DCTQ_ENTRY;  // an allocation: may reach the runtime's rand()
             if (host) (void)hipHostFree(host);
             host = nullptr;
-            LCHK(hipHostMalloc((void **)&host, need, hipHostMallocMapped), "hipHostMalloc(legacy staging)");
-            LCHK(hipHostGetDevicePointer((void **)&dev, host, 0), "hipHostGetDevicePointer");
-            bytes = need;
+            const size_t bytes = need > kStageMin ? need : kStageMin;
+            LCHK(hipHostMalloc((void **)&host, bytes, hipHostMallocMapped), "hipHostMalloc(legacy staging)");
+            LCHK(hipHostGetDevicePointer((void **)&hdev, host, 0), "hipHostGetDevicePointer");
+            host_bytes = bytes;
         }
         return host;
     }
-};
-struct Scratch {
-    unsigned char *dev = nullptr;
-    size_t bytes = 0;
-    unsigned char *get(size_t need) {
-        if (need > bytes) {
-            if (dev) (void)hipFree(dev);
-            dev = nullptr;
-            LCHK(hipMalloc((void **)&dev, need), "hipMalloc(legacy scratch)");
-            bytes = need;
+    unsigned char *dscratch(size_t need) {
+        if (need > scratch_bytes) {
+            DCTQ_ENTRY;
+            if (scratch) (void)hipFree(scratch);
+            scratch = nullptr;
+            LCHK(hipMalloc((void **)&scratch, need), "hipMalloc(legacy scratch)");
+            scratch_bytes = need;
         }
-        return dev;
+        return scratch;
     }
 };
-constexpr int kMaxDevices = 64;
-Staging g_stages[kMaxDevices];
-Scratch g_scratches[kMaxDevices];
-int current_device() {
+
+__global__ void k_nop() {}
+
+std::mutex g_pool_mu;
+std::vector<Lane *> g_pool;  // lanes of threads that have exited
+
+struct ThreadLanes {
+    std::vector<Lane *> lanes;
+    ~ThreadLanes() {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (Lane *l : lanes) g_pool.push_back(l);
+    }
+};
+thread_local ThreadLanes t_lanes;
+
+// This thread's lane on the current device, made (or taken from the pool) on
+// its first call there.
+Lane &lane() {
+    std::optional<dctq::RandIsolation> iso;
+    if (!dctq::runtime_started()) iso.emplace();  // this hipGetDevice may initialise the runtime
     int d = 0;
     LCHK(hipGetDevice(&d), "hipGetDevice");
-    if (d < 0 || d >= kMaxDevices) die("device index out of range");
-    return d;
+    dctq::note_runtime_started();
+    for (Lane *l : t_lanes.lanes)
+        if (l->device == d) return *l;
+    if (!iso) iso.emplace();
+    Lane *l = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i)
+            if (g_pool[i]->device == d) {
+                l = g_pool[i];
+                g_pool.erase(g_pool.begin() + (long)i);
+                break;
+            }
+    }
+    if (!l) {
+        l = new Lane();
+        l->device = d;
+        LCHK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking), "hipStreamCreateWithFlags(legacy lane)");
+        (void)l->stage(kStageMin);
+        hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, l->stream);  // the stream's first queue, under isolation
+        LCHK(hipGetLastError(), "legacy lane launch");
+        LCHK(hipStreamSynchronize(l->stream), "hipStreamSynchronize");
+    }
+    t_lanes.lanes.push_back(l);
+    return *l;
 }
-Staging &stage_buf() { return g_stages[current_device()]; }
-Scratch &scratch_buf() { return g_scratches[current_device()]; }
 
-void finish(const char *what) {
+void finish(const Lane &ln, const char *what) {
     LCHK(hipGetLastError(), what);
-    LCHK(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+    LCHK(hipStreamSynchronize(ln.stream), "hipStreamSynchronize");
 }
 
 void pack(double **a, int n, double *dst) {
@@ -216,26 +267,25 @@ void check_n(int n) {
 }
 
 void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
-    DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int n = ctx->block_size;
     check_n(n);
     const size_t nn = (size_t)n * n;
+    Lane &ln = lane();
     if (4 * nn * sizeof(double) <= (size_t)kLdsBytes) {
-        Staging &sg = stage_buf();
-        double *h = (double *)sg.get(sizeof(double) * 4 * nn);
-        const double *dv = (const double *)sg.dev;
+        double *h = (double *)ln.stage(sizeof(double) * 4 * nn);
+        const double *dv = (const double *)ln.hdev;
         pack(ctx->dct_matrix, n, h);
         pack(ctx->transposed_dct, n, h + nn);
         pack(input, n, h + 2 * nn);
         const int threads = nn < 256 ? (int)((nn + 63) / 64) * 64 : 256;
         const size_t lds = sizeof(double) * 4 * nn;
         if (fwd)
-            hipLaunchKernelGGL(k_transform_small<true>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, dv + 2 * nn,
-                               (double *)dv + 3 * nn);
+            hipLaunchKernelGGL(k_transform_small<true>, dim3(1), dim3(threads), lds, ln.stream, n, dv, dv + nn,
+                               dv + 2 * nn, (double *)dv + 3 * nn);
         else
-            hipLaunchKernelGGL(k_transform_small<false>, dim3(1), dim3(threads), lds, 0, n, dv, dv + nn, dv + 2 * nn,
-                               (double *)dv + 3 * nn);
-        finish("transform launch");
+            hipLaunchKernelGGL(k_transform_small<false>, dim3(1), dim3(threads), lds, ln.stream, n, dv, dv + nn,
+                               dv + 2 * nn, (double *)dv + 3 * nn);
+        finish(ln, "transform launch");
         unpack(h + 3 * nn, n, output);
         return;
     }
@@ -244,40 +294,42 @@ void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
     pack(ctx->dct_matrix, n, h.data());
     pack(ctx->transposed_dct, n, h.data() + nn);
     pack(input, n, h.data() + 2 * nn);
-    double *d = (double *)scratch_buf().get(sizeof(double) * 5 * nn), *t = d + nn, *in = d + 2 * nn, *tmp = d + 3 * nn,
+    double *d = (double *)ln.dscratch(sizeof(double) * 5 * nn), *t = d + nn, *in = d + 2 * nn, *tmp = d + 3 * nn,
            *out = d + 4 * nn;
-    LCHK(hipMemcpy(d, h.data(), sizeof(double) * 3 * nn, hipMemcpyHostToDevice), "hipMemcpy(legacy transform in)");
+    LCHK(hipMemcpyAsync(d, h.data(), sizeof(double) * 3 * nn, hipMemcpyHostToDevice, ln.stream),
+         "hipMemcpy(legacy transform in)");
     const unsigned grid = (unsigned)((nn + 255) / 256);
     if (fwd) {
-        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, in, t, tmp);
-        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, d, tmp, out);
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, ln.stream, n, in, t, tmp);
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, ln.stream, n, d, tmp, out);
     } else {
-        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, t, in, tmp);
-        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, 0, n, tmp, d, out);
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, ln.stream, n, t, in, tmp);
+        hipLaunchKernelGGL(k_pass, dim3(grid), dim3(256), 0, ln.stream, n, tmp, d, out);
     }
     LCHK(hipGetLastError(), "transform launch");
-    LCHK(hipMemcpy(h.data(), out, sizeof(double) * nn, hipMemcpyDeviceToHost), "hipMemcpy(legacy transform out)");
+    LCHK(hipMemcpyAsync(h.data(), out, sizeof(double) * nn, hipMemcpyDeviceToHost, ln.stream),
+         "hipMemcpy(legacy transform out)");
+    LCHK(hipStreamSynchronize(ln.stream), "hipStreamSynchronize");
     unpack(h.data(), n, output);
 }
 
 // One elementwise launch over an n x n block; inputs/outputs as flat host arrays.
 void elementwise(int mode, int n, double **m, int flag, double variance, const double *din, const int *iin,
                  double *dout, int *iout) {
-    DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     const int nn = n * n;
     const size_t bytes = sizeof(double) * 3 * (size_t)nn + sizeof(int) * 2 * (size_t)nn;
-    Staging &sg = stage_buf();
-    unsigned char *h = sg.get(bytes);
+    Lane &ln = lane();
+    unsigned char *h = ln.stage(bytes);
     double *hm = (double *)h, *hd = hm + nn;
     int *hi = (int *)(hd + 2 * nn);
     pack(m, n, hm);
     if (din) memcpy(hd, din, sizeof(double) * nn);
     if (iin) memcpy(hi, iin, sizeof(int) * nn);
-    double *dm = (double *)sg.dev, *dd = dm + nn, *ddo = dd + nn;
+    double *dm = (double *)ln.hdev, *dd = dm + nn, *ddo = dd + nn;
     int *di = (int *)(ddo + nn), *dio = di + nn;
-    hipLaunchKernelGGL(k_elementwise, dim3((nn + 255) / 256), dim3(256), 0, 0, mode, nn, dm, flag, variance, dd, di,
-                       ddo, dio);
-    finish("elementwise launch");
+    hipLaunchKernelGGL(k_elementwise, dim3((nn + 255) / 256), dim3(256), 0, ln.stream, mode, nn, dm, flag, variance,
+                       dd, di, ddo, dio);
+    finish(ln, "elementwise launch");
     if (dout) memcpy(dout, (double *)h + 2 * nn, sizeof(double) * nn);
     if (iout) memcpy(iout, (int *)((double *)h + 3 * nn) + nn, sizeof(int) * nn);
 }
@@ -425,28 +477,30 @@ void dequantize(QuantContext *ctx, int **quant_coeffs, double **dct_coeffs, doub
 }
 
 double calculate_block_variance(double **block, int block_size) {
-    DCTQ_ENTRY;  // HIP calls below must not touch the host's rand() stream
     check_n(block_size);
     const size_t nn = (size_t)block_size * block_size;
+    Lane &ln = lane();
     if (nn * sizeof(double) <= (size_t)kLdsBytes) {
-        Staging &sg = stage_buf();
-        double *hs = (double *)sg.get(sizeof(double) * (nn + 1));
-        double *dv = (double *)sg.dev;
+        double *hs = (double *)ln.stage(sizeof(double) * (nn + 1));
+        double *dv = (double *)ln.hdev;
         pack(block, block_size, hs);
         const int threads = nn < 256 ? (int)((nn + 63) / 64) * 64 : 256;
-        hipLaunchKernelGGL(k_variance_small, dim3(1), dim3(threads), sizeof(double) * nn, 0, (int)nn, dv, dv + nn);
-        finish("variance launch");
+        hipLaunchKernelGGL(k_variance_small, dim3(1), dim3(threads), sizeof(double) * nn, ln.stream, (int)nn, dv,
+                           dv + nn);
+        finish(ln, "variance launch");
         return hs[nn];
     }
-    std::vector<double> h(nn);
+    std::vector<double> h(nn + 1);
     pack(block, block_size, h.data());
-    double *dv = (double *)scratch_buf().get(sizeof(double) * (nn + 1));
-    LCHK(hipMemcpy(dv, h.data(), sizeof(double) * nn, hipMemcpyHostToDevice), "hipMemcpy(variance in)");
-    hipLaunchKernelGGL(k_variance, dim3(1), dim3(1), 0, 0, (int)nn, dv, dv + nn);
+    double *dv = (double *)ln.dscratch(sizeof(double) * (nn + 1));
+    LCHK(hipMemcpyAsync(dv, h.data(), sizeof(double) * nn, hipMemcpyHostToDevice, ln.stream),
+         "hipMemcpy(variance in)");
+    hipLaunchKernelGGL(k_variance, dim3(1), dim3(1), 0, ln.stream, (int)nn, dv, dv + nn);
     LCHK(hipGetLastError(), "variance launch");
-    double v;
-    LCHK(hipMemcpy(&v, dv + nn, sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy(variance out)");
-    return v;
+    LCHK(hipMemcpyAsync(h.data() + nn, dv + nn, sizeof(double), hipMemcpyDeviceToHost, ln.stream),
+         "hipMemcpy(variance out)");
+    LCHK(hipStreamSynchronize(ln.stream), "hipStreamSynchronize");
+    return h[nn];
 }
 
 double **adjust_matrix_for_block(QuantContext *ctx, double variance, int is_quantize) {

@@ -9,9 +9,9 @@ namespace dctq {
 
 constexpr int kWavesP = 4;
 constexpr int kThreadsP = 64 * kWavesP;
-constexpr int kPitchP = 272;
-constexpr int kRtOcc = 4;                    // the fused round trip's waves per SIMD (launch bound)
-constexpr int kRtGridMult = DCTQ_GRID_MULT;  // ... and its grid multiplier (dctq_internal.h)  // bytes per block in the stage: 256 + 16 (b128 writes spread over the banks)
+constexpr int kPitchP = 272;          // bytes per block in the stage: 256 + 16 (b128 writes spread over the banks)
+constexpr int kRtOcc = 4;             // the fused round trip's waves per SIMD (launch bound)
+constexpr int kRtGridMult = kGridMult;  // ... and its grid multiplier (dctq_internal.h)
 
 typedef uint32_t u2p __attribute__((ext_vector_type(2)));
 typedef uint32_t u4p __attribute__((ext_vector_type(4)));
@@ -92,7 +92,7 @@ __device__ __forceinline__ void stage_store(const u4p (&val)[8], int lane, char 
     nbytes = (uint32_t)__builtin_amdgcn_readfirstlane(nbytes);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)nbytes, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
+    for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, kNtAux);
 }
 __device__ __forceinline__ void store_stage(const uint4 *stage, int wv, int lane, char *dst, uint32_t nbytes) {
     u4p val[8];

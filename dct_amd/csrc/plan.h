@@ -8,7 +8,7 @@
 
 struct dctq_plan {
     int quality, adaptive, device, num_cus;
-    int variant;                 // 2: dispatch by launch size; others only via libdct_amd_diag.so
+    int variant;                 // 2: the product kernels; 1 / 4 only through the dctq_diag_* entry points
     dctq::FastTables fast;       // thresholds for the mode in `adaptive`
     dctq::DevTables host;        // host copy of the device tables
     dctq::DevTables *dev;        // device copy
@@ -41,20 +41,6 @@ int max_abs_quantized(const DevTables &t);
 // the admission tolerance of that bound (== idct8_bound.h kInvTol; api.hip checks they agree)
 constexpr double kInvTolDiag = 5e-5;
 namespace dctq {
-}  // namespace dctq
-
-namespace dctq {
-// Kernel variants only the diagnostic library carries (fdct8_diag.hip fills this
-// when libdct_amd_diag.so loads; all null in libdct_amd.so, whose plans cannot
-// select a variant): the v1 / v2 forwards (variants 1 / 4) and the lane-per-block
-// fp64 float forward and inverse (variant 1).
-struct DiagKernels {
-    int (*forward_quant)(const dctq_plan *plan, const PlaneSet &ps, hipStream_t stream);
-    hipError_t (*forward_float)(const PlaneArgs &p, const DevTables *dev, float *coef, hipStream_t stream);
-    hipError_t (*inverse)(const DevTables *dev, int adaptive, const int16_t *coef, const int32_t *var_num,
-                          long long nblk, float *recon, hipStream_t stream);
-};
-extern DiagKernels g_diag_kernels;
 }  // namespace dctq
 
 #define HIPCHK(call, what)                                               \

@@ -31,9 +31,7 @@
 
 namespace dctq {
 
-#ifndef DCTQ_COUNT_POLICY
-#define DCTQ_COUNT_POLICY 2  // count's tile loads: non-temporal (A/B knob)
-#endif
+constexpr int kCountPolicy = kNtAux;  // count's tile loads: non-temporal (read once)
 constexpr int kRleWaves = 4;
 constexpr int kRleThreads = 64 * kRleWaves;
 
@@ -84,7 +82,7 @@ __global__ __launch_bounds__(kRleThreads) void rle_count_kernel(const int16_t *_
             const_cast<int16_t *>(coef) + tt * 64 * 64, (short)0, nb * 128, 0x00020000);  // past the tail: zeros
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, DCTQ_COUNT_POLICY);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, k * 1024, kCountPolicy);
             q[k] = make_uint4(v[0], v[1], v[2], v[3]);
         }
     };
@@ -237,15 +235,8 @@ constexpr uint8_t kZzStatic[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 2
                                    58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 constexpr int kEmitPitch = 144;  // LDS bytes per block (128 + 16: lane-per-block row reads are conflict-free)
 constexpr int kEmitLds = 64 * kEmitPitch;
-#ifdef DCTQ_RLE_WAVE_ONLY  // A/B switch (tools/rle_ab.py): emit tiles take the wave path, decode halves the quad path
-constexpr uint32_t kLaneWalkMax = 0;
-#else
-#ifndef DCTQ_EMIT_WALK_MAX
-#define DCTQ_EMIT_WALK_MAX 2048
-#endif
-constexpr uint32_t kLaneWalkMax = DCTQ_EMIT_WALK_MAX;  // symbols of a tile the lane-per-block path stages
+constexpr uint32_t kLaneWalkMax = 2048;  // symbols of a tile the lane-per-block path stages
 static_assert(kLaneWalkMax <= kEmitLds / 4 && kLaneWalkMax <= 2048, "two flush rounds of 1 024");
-#endif
 // 2-byte symbols: every tile fits the staging (64 x 64 symbols + one unit of padding in the
 // 9 KiB), so every tile takes the lane-per-block path -- dense ones too: -5.8 % on the bench's
 // encode step against the wave path above 2 048 (profiles/r05/encode_walk4k_ab.log)
@@ -450,7 +441,7 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
 // ---- decode: one wave per 64-block tile, rebuilt 32 blocks at a time in a
 // natural-order LDS copy (8 waves/SIMD) and written as 1 KiB stores (8
 // lane-addresses per block).  Each half takes one of three paths by its symbol
-// count: lane (<= 240), walk (<= DCTQ_DEC_WALK_MAX) or quad (denser halves);
+// count: lane (<= 240), walk (<= kDecWalkMax) or quad (denser halves);
 // all three place each symbol at zigzag position pos (run_length_decode: pos +=
 // run; zigzag[pos++] = value, dropped past the end, src/entropy.c:327-351) of
 // its block's natural-order row (zigzag_to_block, :183-210, through an LDS copy
@@ -459,9 +450,6 @@ __global__ __launch_bounds__(kRleThreads, 4) void rle_emit_kernel(const int16_t 
 // stream.  Each half tile's LDS work starts after a vmcnt(0) that retires the
 // previous half's stores (store-data hazard); no store is issued inside the half.
 constexpr int kHalf = 32;
-#ifndef DCTQ_DEC_WALK_MAX
-#define DCTQ_DEC_WALK_MAX 1024
-#endif
 
 // offv: lane b holds offsets[64t + b] (b < nb); oend = offsets[64t + nb], the end
 // of the tile's symbols (lane 64 does not exist, and readlane(64) would wrap).
@@ -486,11 +474,7 @@ __device__ __forceinline__ uint32_t off_at(uint32_t offv, uint32_t oend, int b) 
 // density (one coalesced load per 64 symbols instead of per-lane 16-B loads).
 //
 // 4 KiB + 960 B per wave keeps 8 waves/SIMD (the scan path needs them).
-#ifdef DCTQ_RLE_WAVE_ONLY
-constexpr uint32_t kDecLaneMax = 0, kDecWalkMax = 0;
-#else
-constexpr uint32_t kDecLaneMax = 240, kDecWalkMax = DCTQ_DEC_WALK_MAX;
-#endif
+constexpr uint32_t kDecLaneMax = 240, kDecWalkMax = 1024;
 constexpr int kDecPitch = 144;
 constexpr int kDecBatch = 16;  // symbols per lane per step
 constexpr int kDecLds = kHalf * 128 + 240 * 4;  // >= kHalf * kDecPitch
@@ -716,7 +700,7 @@ __global__ __launch_bounds__(kRleThreads, W == 4 ? 8 : 7) void rle_decode_kernel
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(coef + (b0 + h) * 64, (short)0, (he - h) * 128, 0x00020000);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, DCTQ_NT_AUX);
+            for (int k = 0; k < 4; ++k) __builtin_amdgcn_raw_buffer_store_b128(val[k], rs, lane * 16, k * 1024, kNtAux);
         }
     }
 }

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
         prefetch_batch<false, kRtBufRows>(ps, g + step, lane, nxt);
         const BatchOut out = batch_out(ps, k, b);  // resolved before the fences (fdct8_core.h)
         char *recon = reinterpret_cast<char *>(rt.recon[k]) + (size_t)b * 64 * 256;
-        if (DCTQ_PIN_OUT) asm volatile("" : "+s"(recon));
+        asm volatile("" : "+s"(recon));
 
         // ---- 1. forward into the stage; ties resolved in place
         int32_t var_num;
@@ -283,11 +283,11 @@ __global__ __launch_bounds__(kThreads, kRtOcc) void roundtrip8(RoundTripSet rt, 
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(out.base, (short)0, (int)(nb * 128u), 0x00020000);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, DCTQ_NT_AUX);
+            for (int c = 0; c < 8; ++c) __builtin_amdgcn_raw_buffer_store_b128(val[c], rs, lane * 16, c * 1024, kNtAux);
             if (VAR) {
                 const __amdgpu_buffer_rsrc_t rv =
                     __builtin_amdgcn_make_buffer_rsrc(out.var, (short)0, (int)(nb * 4u), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, DCTQ_NT_AUX);
+                __builtin_amdgcn_raw_buffer_store_b32(var_num, rv, lane * 4, 0, kNtAux);
             }
         }
 

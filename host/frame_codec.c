@@ -14,6 +14,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "dct_amd.h"
 
@@ -98,14 +99,18 @@ int main(int argc, char **argv) {
     CHK(dctq_malloc(&off, (size_t)(nblk + 1) * 4));
     CHK(dctq_malloc(&sym, (size_t)cap * 4));
     CHK(dctq_malloc(&ws, dctq_encode_workspace_bytes(nblk)));
-    CHK(dctq_encode_planes(plan, &pl, 1, &c2p, (uint32_t *)off, (uint32_t *)sym, cap, ws, NULL));
+    /* the most compact format the plan admits (include/dct_amd.h): dctq_encode_planes16's
+       2-byte symbols are widened to the 4-byte (uint16)value | run << 16 here, so the digest
+       is format-independent; the 4-byte entry point's stream must be the same */
+    const int symbytes = dctq_plan_symbol_bytes(plan);
+    if (symbytes == 2)
+        CHK(dctq_encode_planes16(plan, &pl, 1, &c2p, (uint32_t *)off, (uint16_t *)sym, cap, ws, NULL));
+    else
+        CHK(dctq_encode_planes(plan, &pl, 1, &c2p, (uint32_t *)off, (uint32_t *)sym, cap, ws, NULL));
     CHK(dctq_synchronize(NULL));
     uint32_t total = 0;
     CHK(dctq_memcpy_dtoh(&total, (const char *)off + (size_t)nblk * 4, 4));
     uint32_t *hs = malloc((size_t)total * 4 + 4);
-    /* the plan's symbol format (include/dct_amd.h): 2-byte symbols are widened to the
-       4-byte (uint16)value | run << 16 here, so the digest is format-independent */
-    const int symbytes = dctq_plan_symbol_bytes(plan);
     CHK(dctq_memcpy_dtoh(hs, sym, (size_t)total * symbytes));
     if (symbytes == 2) {
         const uint16_t *h16 = (const uint16_t *)hs;
@@ -115,7 +120,18 @@ int main(int argc, char **argv) {
             const uint32_t run = u ? u >> 10 : 64u;
             hs[i] = ((uint32_t)value & 0xFFFFu) | run << 16;
         }
+        /* the default entry point: 4-byte symbols for every plan (DCTQ_ABI_VERSION 6) */
+        void *sym4;
+        CHK(dctq_malloc(&sym4, (size_t)cap * 4));
+        CHK(dctq_encode_planes(plan, &pl, 1, &c2p, (uint32_t *)off, (uint32_t *)sym4, cap, ws, NULL));
+        CHK(dctq_synchronize(NULL));
+        uint32_t *h4 = malloc((size_t)total * 4 + 4);
+        CHK(dctq_memcpy_dtoh(h4, sym4, (size_t)total * 4));
+        printf("symbols4_equal:%d\n", memcmp(h4, hs, (size_t)total * 4) == 0);
+        free(h4);
+        CHK(dctq_free(sym4));
     }
+    printf("abi_version:%d\n", dctq_abi_version());
     printf("symbol_bytes:%d\n", symbytes);
     uint64_t fs = 1469598103934665603ULL;
     const uint8_t *sb = (const uint8_t *)hs;

@@ -27,6 +27,13 @@
 extern "C" {
 #endif
 
+/* ABI revision of this header.  6: dctq_encode_planes writes 4-byte symbols for
+ * every plan again (round 5 had switched plans with |q| <= 511 to 2-byte symbols
+ * under the same entry point); the 2-byte format is dctq_encode_planes16, opt-in;
+ * dctq_abi_version() returns the library's revision so a host can check both. */
+#define DCTQ_ABI_VERSION 6
+int dctq_abi_version(void);
+
 #define DCTQ_OK 0
 #define DCTQ_EINVAL (-1)   /* bad argument (sizes not multiples of 8, misaligned, ...) */
 #define DCTQ_EHIP (-2)     /* a HIP runtime call failed (dctq_error_string has the detail) */
@@ -100,16 +107,7 @@ int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int 
  *   offsets[b]  = first symbol of block b, offsets[N] = total symbols
  *   symbols[..] = the reference's run_length_encode of every block, in order
  *                 (as dctq_rle_count + dctq_rle_emit over the concatenated
- *                 coefficient planes), in the plan's symbol format
- *                 (dctq_plan_symbol_bytes):
- *                   4 (uint32_t): (uint16_t)value | run << 16;
- *                   2 (uint16_t): (run & 63) << 10 | (value & 0x3FF), value
- *                     in [-511, 511] -- every plan whose quantization table
- *                     bounds each quantized coefficient there (q <= 90 of the
- *                     standard table): half the bytes; dctq_rle_decode16 reads
- *                     it.  Runs are 0..63 except the one symbol of an all-zero
- *                     block, (value 0, run 64), which is 0x0000 (no other
- *                     symbol is: a zero value only ends a block, with run >= 1).
+ *                 coefficient planes): uint32_t (uint16_t)value | run << 16.
  * The symbol count is fused into the forward launch.  Symbols at index >=
  * symbols_capacity are not written; offsets are always complete (compare
  * offsets[N] with the capacity).  symbols == NULL or capacity 0: coefficients
@@ -117,9 +115,21 @@ int dctq_round_trip_planes(const dctq_plan *plan, const dctq_plane *planes, int 
  * workspace: dctq_encode_workspace_bytes(N) bytes. */
 size_t dctq_encode_workspace_bytes(long long total_blocks);
 int dctq_encode_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
-                       uint32_t *offsets, void *symbols, long long symbols_capacity, void *workspace,
+                       uint32_t *offsets, uint32_t *symbols, long long symbols_capacity, void *workspace,
                        void *stream);
-/* Bytes per symbol of the plan's encoder output: 2 or 4 (see dctq_encode_planes). */
+/* The same stream in 2-byte symbols (opt-in, half the bytes):
+ *   uint16_t (run & 63) << 10 | (value & 0x3FF), value in [-511, 511];
+ * runs are 0..63 except the one symbol of an all-zero block, (value 0, run 64),
+ * which is 0x0000 (no other symbol is: a zero value only ends a block, with
+ * run >= 1).  dctq_rle_decode16 reads it.  Only for plans whose quantization
+ * table bounds every quantized coefficient by 511 (dctq_plan_symbol_bytes == 2;
+ * q <= 90 of the standard table); DCTQ_EINVAL for the others.  capacity in
+ * symbols; symbols 4-byte aligned. */
+int dctq_encode_planes16(const dctq_plan *plan, const dctq_plane *planes, int nplanes, int16_t *const *coef,
+                         uint32_t *offsets, uint16_t *symbols, long long symbols_capacity, void *workspace,
+                         void *stream);
+/* The most compact symbol format the plan admits: 2 (dctq_encode_planes16 may be
+ * used) or 4 (dctq_encode_planes only). */
 int dctq_plan_symbol_bytes(const dctq_plan *plan);
 
 /* Forward DCT only, float coefficients coef[f][by][bx][64]
@@ -151,7 +161,7 @@ int dctq_rle_emit(const int16_t *coef, long long nblocks, const uint32_t *offset
 /* The inverse, run_length_decode (src/entropy.c:327-351) + zigzag_to_block
  * (:183-210) of every block: coef[b][64] from symbols[offsets[b] ..).
  * dctq_rle_decode16: the same from 2-byte symbols ((run & 63) << 10 | (value &
- * 0x3FF), 0x0000 = (0, 64); a 2-byte plan's dctq_encode_planes output);
+ * 0x3FF), 0x0000 = (0, 64); dctq_encode_planes16's output);
  * symbols 4-byte aligned. */
 int dctq_rle_decode16(const uint16_t *symbols, const uint32_t *offsets, long long nblocks, int16_t *coef,
                       void *stream);
@@ -176,9 +186,12 @@ int dctq_huffman_bits(const int16_t *coef, long long nblocks, uint32_t *bits, vo
 int dctq_huffman_bits_planes(const dctq_plan *plan, const dctq_plane *planes, int nplanes, uint32_t *bits,
                              void *stream);
 
-/* No-op, kept for ABI compatibility: until round 4 it freed the per-stream
- * tie-path stash of the forward's queue kernel, which the product no longer
- * launches (it lives on in the diagnostic build only).  Returns DCTQ_OK. */
+/* The calling thread forgets `stream` (call it before hipStreamDestroy): the
+ * library keeps no per-stream device memory, only each thread's list of the
+ * streams it has launched on, and a stream later created at the same handle
+ * then gets its first call isolated again (that list is also keyed by the
+ * runtime's stream id, so hosts that skip this call stay correct wherever the
+ * runtime tells the two streams apart).  Returns DCTQ_OK. */
 int dctq_stream_release(void *stream);
 
 /* Optional diagnostics: if non-NULL, *counter (device, uint64) is incremented

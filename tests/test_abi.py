@@ -60,10 +60,23 @@ def test_diagnostic_library_exports(lib):
 
 
 def test_no_runtime_knobs_in_product():
-    """Kernel selection is not read from the environment: no getenv in the library sources."""
+    """Kernel selection is not read from the environment: no getenv in the library sources.
+    VERDICT r05 item 6: no compile-time A/B switches in the product sources either (every product
+    value is a constexpr; the diagnostic-only DCTQ_ABLATE lives in fdct8_diag.hip), and no
+    diagnostic dispatch table behind the product entry points."""
+    import re
     csrc = os.path.join(ROOT, "dct_amd", "csrc")
     for f in os.listdir(csrc):
         assert "getenv" not in open(os.path.join(csrc, f)).read(), f
+    product = ["fdct8.hip", "roundtrip.hip", "encode.hip", "rle.hip", "huffman.hip", "api.hip", "legacy.hip",
+               "f64_pair.hip", "fdct8_aux.hip", "fdct8_core.h", "pair_core.h", "scan_core.h", "dctq_internal.h",
+               "plan.h", "aan_f64.h", "zigzag.h", "host_tables.h"]
+    for f in product:
+        src = open(os.path.join(csrc, f)).read()
+        knobs = [m.group(0) for m in re.finditer(r"^#\s*(?:ifndef|ifdef|if|elif)\b.*DCTQ_\w+", src, flags=re.M)
+                 if not re.search(r"DCTQ_\w+_H_?\s*$", m.group(0))]
+        assert not knobs, (f, knobs)
+        assert "g_diag_kernels" not in src and "DiagKernels" not in src, f
 
 
 def test_host_tables_match_reference(lib, blocks):

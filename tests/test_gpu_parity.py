@@ -416,30 +416,136 @@ def test_batched_calls_do_not_serialise_and_leave_rand_alone(T, dm):
     T.cuda.synchronize()
 
 
+class _RawStream:
+    """A raw hipStream_t handle as a stream argument (Plan methods read .cuda_stream)."""
+
+    def __init__(self, handle):
+        self.cuda_stream = handle
+
+
+def _hip():
+    """The HIP runtime this process loaded (PyTorch's libamdhip64.so.7, shared with libdct_amd.so)."""
+    hip = C.CDLL("libamdhip64.so.7")
+    hip.hipStreamCreate.argtypes = [C.POINTER(C.c_void_p)]
+    hip.hipStreamCreate.restype = C.c_int
+    hip.hipStreamDestroy.argtypes = [C.c_void_p]
+    hip.hipStreamDestroy.restype = C.c_int
+    return hip
+
+
+class _HostRandShield:
+    """The test's OWN HIP calls (stream create / destroy) with glibc's random state
+    swapped out, so that only the library's calls can disturb the host's sequence."""
+
+    def __init__(self, libc):
+        self.libc = libc
+        self.libc.setstate.restype = C.c_void_p
+        self.libc.setstate.argtypes = [C.c_void_p]
+        self.libc.initstate.restype = C.c_void_p
+        self.libc.initstate.argtypes = [C.c_uint, C.c_void_p, C.c_size_t]
+        self.buf = C.create_string_buffer(256)
+        self.first = True
+
+    def __enter__(self):
+        if self.first:
+            self.saved = self.libc.initstate(7, self.buf, 256)
+            self.first = False
+        else:
+            self.saved = self.libc.setstate(self.buf)
+
+    def __exit__(self, *exc):
+        self.libc.setstate(self.saved)
+        return False
+
+
 def test_many_streams_rand_and_results(T, dm):
-    """A host that keeps creating streams: past 64 (device, stream) pairs a thread's
-    list of streams it has launched on is cleared (LaunchIsolation) and each stream's
-    next first call is isolated again -- every result stays bit-exact, and glibc's
-    seed-1 sequence drawn between the launches is undisturbed."""
+    """a host that keeps creating streams.  150 DISTINCT raw streams
+    (hipStreamCreate; torch.cuda.Stream() recycles a pool of 32), all alive at once:
+    past 64 (device, stream) pairs a thread's launch-isolation list is cleared and
+    each stream's next first call is isolated again -- every result stays bit-exact,
+    and glibc's seed-1 sequence drawn between the launches is undisturbed."""
     libc = C.CDLL("libc.so.6")
     libc.rand.restype = C.c_int
     libc.srand(1)
-    want = [libc.rand() for _ in range(300)]
+    want = [libc.rand() for _ in range(600)]
+    hip = _hip()
+    shield = _HostRandShield(libc)
+    L = dm.lib()
     plan = dm.Plan(50, 0)
     px = dm.synth(4040, "uniform", 256, 128, 1)
     ref = plan.forward_quant(px)
     T.cuda.synchronize()
-    libc.srand(1)
-    got, outs, streams = [], [], []
-    for i in range(150):
-        st = T.cuda.Stream()
-        streams.append(st)
-        outs.append(plan.forward_quant(px, stream=st))
-        got.append(libc.rand())
-        got.append(libc.rand())
+    outs = [T.empty_like(ref) for _ in range(150)]
+    handles = []
+    with shield:
+        for _ in range(150):
+            h = C.c_void_p()
+            assert hip.hipStreamCreate(C.byref(h)) == 0
+            handles.append(h.value)
+    assert len(set(handles)) == 150
     T.cuda.synchronize()
-    assert got == want
+    libc.srand(1)
+    got = []
+    for rep in range(2):  # the second pass runs after the list was cleared by the first
+        for h, o in zip(handles, outs):
+            plan.forward_quant(px, out=o, stream=_RawStream(h))
+            got.append(libc.rand())
+    for h in handles:
+        dm._check(L.dctq_synchronize(C.c_void_p(h)), L)
+    assert got == want[:len(got)]
     assert all(T.equal(o, ref) for o in outs)
+    for h in handles:  # the host protocol before hipStreamDestroy (include/dct_amd.h)
+        dm._check(L.dctq_stream_release(C.c_void_p(h)), L)
+    with shield:
+        for h in handles:
+            assert hip.hipStreamDestroy(C.c_void_p(h)) == 0
+
+
+def test_stream_handle_reuse_is_isolated(T, dm):
+    """streams destroyed and re-created in a loop.  The runtime
+    hands out a destroyed stream's handle again; a re-created stream's first call
+    must still be isolated (LaunchIsolation keys on the handle AND the runtime's
+    stream id where the runtime has hipStreamGetId, and dctq_stream_release drops
+    the calling thread's entry).  Both host styles -- calling dctq_stream_release
+    before hipStreamDestroy, and not -- keep glibc's seed-1 sequence intact with
+    bit-exact results on every stream."""
+    libc = C.CDLL("libc.so.6")
+    libc.rand.restype = C.c_int
+    libc.srand(1)
+    want = [libc.rand() for _ in range(2000)]
+    hip = _hip()
+    has_id = hasattr(hip, "hipStreamGetId")
+    shield = _HostRandShield(libc)
+    L = dm.lib()
+    plan = dm.Plan(90, 1)
+    px = dm.synth(4141, "smooth", 128, 64, 1)
+    ref = plan.forward_quant(px)
+    T.cuda.synchronize()
+    out = T.empty_like(ref)
+    libc.srand(1)
+    got, seen, reused = [], set(), 0
+    styles = ("release",) + (("no-release",) if has_id else ())
+    for style in styles:
+        for i in range(60):
+            with shield:
+                h = C.c_void_p()
+                assert hip.hipStreamCreate(C.byref(h)) == 0
+            reused += h.value in seen
+            seen.add(h.value)
+            out.zero_()
+            T.cuda.synchronize()
+            plan.forward_quant(px, out=out, stream=_RawStream(h.value))
+            got.append(libc.rand())
+            plan.forward_quant(px, out=out, stream=_RawStream(h.value))  # the steady-state call
+            got.append(libc.rand())
+            dm._check(L.dctq_synchronize(C.c_void_p(h.value)), L)
+            assert T.equal(out, ref), (style, i)
+            if style == "release":
+                dm._check(L.dctq_stream_release(C.c_void_p(h.value)), L)
+            with shield:
+                assert hip.hipStreamDestroy(h) == 0
+    assert reused > 0, "the runtime never reused a stream handle: nothing was exercised"
+    assert got == want[:len(got)]
 
 
 class _PerThreadStream:
@@ -1334,8 +1440,53 @@ def test_c_host_programs(T, dm, blocks, tmp_path):
             fs = ((fs ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
         assert int(got["symbols"]) == wsym.size and int(got["symbols_fnv1a"], 16) == fs, (w, h, q, ad)
         assert int(got["symbol_bytes"]) == dm.symbol_bytes(q, ad) == 2, (w, h, q, ad)
+        # the default entry point keeps the 4-byte format for every plan (ABI 6)
+        assert got["symbols4_equal"] == "1" and int(got["abi_version"]) == 6, got
         want_bits = int(O.huffman_bits_plane(np.frombuffer(want, np.int16).reshape(-1, 64)).astype(np.uint64).sum())
         assert int(got["huffman_bits"]) == want_bits, (w, h, q, ad)
+
+
+def _run_mt(root, pxfile, w, h, q, ad, threads, reps, out):
+    import subprocess
+    r = subprocess.run([os.path.join(root, "host", "block_pipeline_mt"), str(pxfile), str(w), str(h), str(q), str(ad),
+                        str(threads), str(reps), str(out)], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr
+    return dict(l.split(":", 1) for l in r.stdout.strip().splitlines())
+
+
+def test_legacy_threads_overlap(T, dm, tmp_path):
+    """the per-block drop-in from 8 host threads over ONE shared
+    DCTContext / QuantContext (host/block_pipeline_mt.c: the 5-call pipeline of
+    host/block_pipeline.c per block).  Each thread has its own stream and staging
+    buffer (legacy.hip lanes) and takes no lock after its first call: bit-exact
+    quantized ints and reconstructions (oracle), identical to one thread, >= 3x the
+    one-thread pipeline rate, and glibc's seed-1 rand() sequence drawn by the main
+    thread while the workers run is undisturbed."""
+    import subprocess
+    import oracle as O
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run(["make", "-C", os.path.join(root, "host")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    w, h, q, ad = 256, 128, 50, 1
+    px = O.synth_plane(4321, O.KINDS["smooth"], w, h)
+    pxfile = tmp_path / "px.u8"
+    px.tofile(pxfile)
+    rec = np.dtype([("q", "<i4", 64), ("r", "<f8", 64)])
+    want_q = O.forward_plane(px, q, ad).astype(np.int32)
+    want_r = O.inverse_plane(want_q, q, ad, O.plane_variance(px))
+    res = {}
+    for threads in (1, 8):
+        f = tmp_path / f"out{threads}.bin"
+        res[threads] = _run_mt(root, pxfile, w, h, q, ad, threads, 3, f)
+        got = np.fromfile(f, rec)
+        assert np.array_equal(got["q"], want_q), threads
+        assert np.array_equal(got["r"].view(np.uint64), want_r.view(np.uint64)), threads  # bit-exact doubles
+        assert res[threads]["rand_ok"] == "1", res[threads]
+    assert (tmp_path / "out1.bin").read_bytes() == (tmp_path / "out8.bin").read_bytes()
+    assert int(res[8]["rand_draws"]) > 1000, res[8]
+    r1, r8 = float(res[1]["pipelines_per_s"]), float(res[8]["pipelines_per_s"])
+    print(f"legacy per-block pipeline: 1 thread {r1:.0f}/s, 8 threads {r8:.0f}/s ({r8 / r1:.2f}x)")
+    assert r8 >= 3.0 * r1, (r1, r8)
 
 
 @pytest.mark.parametrize("prog", ["dct", "quantization", "entropy"])
@@ -1641,6 +1792,15 @@ def test_encode_planes_fused(T, dm):
                 assert np.array_equal(sym.cpu().numpy().view(np.uint32), wsym), (q, ad)
             # and back: the decoder of the stream's format restores every block
             assert np.array_equal(dm.rle_decode(sym, off).cpu().numpy(), want), (q, ad)
+            # dctq_encode_planes writes the 4-byte format for EVERY plan (ABI 6);
+            # the 2-byte format is dctq_encode_planes16, refused where values can exceed 511
+            _, off4, sym4 = plan.encode_planes([gpu_px(T, p) for p in planes], symbol_bytes=4)
+            assert sym4.dtype == T.int32 and np.array_equal(sym4.cpu().numpy().view(np.uint32), wsym), (q, ad)
+            assert T.equal(off4, off)
+            if plan.symbol_bytes == 4:
+                with pytest.raises(dm.DctqError):
+                    plan.encode_planes([gpu_px(T, p) for p in planes], symbol_bytes=2)
+    assert dm.lib().dctq_abi_version() == 6
 
 
 def test_encode_capacity_and_large(T, dm):
@@ -1663,6 +1823,27 @@ def test_encode_capacity_and_large(T, dm):
             _, off2, sym2 = plan.encode_planes([px], capacity=cap)
             assert np.array_equal(off.cpu().numpy(), off2.cpu().numpy())
             assert sym2.numel() == cap and np.array_equal(sym2.cpu().numpy(), sym[:cap].cpu().numpy()), (kind, cap)
+        # nothing at or past the capacity is written, in either format: the stream goes
+        # into a LARGER buffer pre-filled with a sentinel, odd and even caps, tiles at odd offsets
+        L = dm.lib()
+        descs = (dm._Plane * 1)(dm.plane_desc(px))
+        nb = px.shape[-1] // 8 * (px.shape[-2] // 8)
+        coef = T.empty((nb, 64), dtype=T.int16, device="cuda")
+        cp = (C.c_void_p * 1)(coef.data_ptr())
+        offs = T.empty(nb + 1, dtype=T.int32, device="cuda")
+        ws = T.empty(int(L.dctq_encode_workspace_bytes(nb)) // 4 + 1, dtype=T.int32, device="cuda")
+        odd_tile = int(off[65].item())
+        for sb, fn, dt in ((2, L.dctq_encode_planes16, T.int16), (4, L.dctq_encode_planes, T.int32)):
+            full = (sym if sym.dtype == dt else plan.encode_planes([px], symbol_bytes=sb)[2]).cpu().numpy()
+            for cap in (total // 3, total // 3 + 1, tile_end - 1, tile_end, tile_end + 1, odd_tile, odd_tile + 1,
+                        total - 1, 1, 2, 3):
+                buf = T.full((cap + 64,), 0x5A5A, dtype=dt, device="cuda")
+                dm._check(fn(plan._h, descs, 1, C.cast(cp, C.c_void_p), C.c_void_p(offs.data_ptr()),
+                             C.c_void_p(buf.data_ptr()), cap, C.c_void_p(ws.data_ptr()), None), L)
+                T.cuda.synchronize()
+                got = buf.cpu().numpy()
+                assert np.array_equal(got[:cap], full[:cap]), (q, kind, sb, cap)
+                assert (got[cap:] == 0x5A5A).all(), (q, kind, sb, cap, np.nonzero(got[cap:] != 0x5A5A)[0][:8])
     plan = dm.Plan(50, 0)
     luma = dm.synth(13, "uniform", 3840, 2160, 5)
     chroma = dm.synth(14, "smooth", 1920, 1080, 3)
