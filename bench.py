@@ -702,6 +702,44 @@ def small_frame_leg(args, plan, dev):
     return res
 
 
+def legacy_leg(args, dev, threads=(1, 8)):
+    """The reference's per-block API served by libdct_amd.so (include/dct.h,
+    include/quantization.h): host/block_pipeline_mt.c runs the reference's forward
+    loop (create_block_from_pixels -> dct_forward -> calculate_block_variance ->
+    quantize, tests/test_entropy.c:300-316) over every block of one 256x128 plane
+    from 1 and from 8 host threads sharing one context (legacy.hip: a lane per
+    thread, no lock after a thread's first call), a child process of its own.
+    Latency-bound by design (one block per call, as in the reference); reported
+    next to the reference's one-thread CPU rate as a stated baseline, not a target.
+    Self-checked: the 8-thread output equals the 1-thread output."""
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "host", "block_pipeline_mt")
+    if not os.path.exists(exe):
+        raise RuntimeError(f"{exe} is not built (make -C host)")
+    w, h = 256, 128
+    px = dct_amd.synth(args.seed + 31, args.kind, w, h, device=dev)[0].cpu().numpy()
+    res = {"op": "reference per-block forward loop through the legacy C API (host/block_pipeline_mt.c), "
+                 f"{w}x{h} plane, q{args.quality} adaptive={args.adaptive}", "blocks": (w // 8) * (h // 8)}
+    with tempfile.TemporaryDirectory() as tmp:
+        pf = os.path.join(tmp, "px.u8")
+        px.tofile(pf)
+        outs = {}
+        for t in threads:
+            of = os.path.join(tmp, f"out{t}.bin")
+            r = subprocess.run([exe, pf, str(w), str(h), str(args.quality), str(args.adaptive), str(t), "4", of,
+                                "forward"], capture_output=True, text=True, timeout=120)
+            if r.returncode != 0:
+                raise RuntimeError(f"block_pipeline_mt {t} threads: rc {r.returncode}: {r.stderr[-500:]}")
+            kv = dict(ln.split(":", 1) for ln in r.stdout.strip().splitlines())
+            outs[t] = open(of, "rb").read()
+            res[f"threads_{t}"] = {"blocks_per_s": float(kv["pipelines_per_s"]), "calls_per_s": float(kv["calls_per_s"]),
+                                   "rand_undisturbed": kv["rand_ok"] == "1"}
+    res["threads_equal_output"] = len(set(outs.values())) == 1
+    res["scaling_8_over_1"] = res["threads_8"]["blocks_per_s"] / res["threads_1"]["blocks_per_s"]
+    return res
+
+
 def encode_leg(args, plan, luma, chroma, world, dev):
     """the encoder over the frame stream -- dctq_encode_planes16
     (2-byte symbols, where the plan admits them; else dctq_encode_planes) (forward + zigzag run-length symbols of reference semantics, the symbol count
@@ -1235,6 +1273,7 @@ def main():
                      "bytes_per_launch": avg_launch_bytes, "movement_ceiling": None},
         "cpu_baseline": None, "parity_check": None, "parity_error": None,
         "gather": None, "band": None, "round_trip": None, "encode": None, "small_frame": None,
+        "legacy_per_block": None,
         "gpu": None, "build": build_record(),
         "note": "u8 pixels in, int16 coefficients out; fp32 AAN butterfly with the exact fp64 "
                 "reference-order recomputation for guard-band (tie) coefficients",
@@ -1251,6 +1290,7 @@ def main():
             collective=False)
     if world == 1 and not args.no_cpu:  # single-GPU config
         out["small_frame"] = legs.run("small_frame", lambda: small_frame_leg(args, plan, dev), collective=False)
+        out["legacy_per_block"] = legs.run("legacy_per_block", lambda: legacy_leg(args, dev), collective=False)
     encode = None
     if args.encode_steps > 0:  # its timing takes the max over ranks: collective at N>1
         encode = legs.run("encode", lambda: encode_leg(args, plan, luma, chroma, world, dev))
@@ -1288,6 +1328,9 @@ def main():
             res = legs.run("cpu", lambda: cpu_leg(args, world, fwd_check, huf_check, rt_check), collective=False)
             cpu, parity = res if res is not None else (None, None)
             out["cpu_baseline"] = cpu
+            lp = out.get("legacy_per_block")
+            if cpu and lp:  # the stated baseline beside it: the reference's own loop on one CPU thread
+                lp["reference_cpu_one_thread_blocks_per_s"] = cpu["builds"]["O2_one_thread"]["blocks_per_s"]
             if parity is not None:
                 out["parity_check"], out["parity_error"] = parity.get("forward"), parity.get("error")
                 if encode:

@@ -7,8 +7,10 @@
  * src/quantization.c:8; SURVEY 8(b) ran 8 pthreads over one context).  Linked
  * against libdct_amd.so instead of src/{dct,quantization}.c.
  *
- *   block_pipeline_mt <pixels.u8> <width> <height> <quality> <adaptive> <threads> <reps> <out>
+ *   block_pipeline_mt <pixels.u8> <width> <height> <quality> <adaptive> <threads> <reps> <out> [forward]
  *
+ * With "forward" the pipeline stops after quantize (the four calls of the
+ * reference's forward loop, tests/test_entropy.c:300-316; recon reads 0).
  * Thread t takes block rows t, t + T, ...; every rep repeats the whole plane.
  * <out> receives, per block in raster order, the 64 quantized ints (int32) and
  * the 64 reconstructed doubles (dct_inverse output, before + 128).  While the
@@ -30,7 +32,7 @@
 
 typedef struct {
     const unsigned char *px;
-    int width, height, threads, reps, tid;
+    int width, height, threads, reps, tid, forward_only;
     DCTContext *dct;
     QuantContext *qc;
     int32_t *q_out;
@@ -59,8 +61,10 @@ static void pipeline(Job *j, int by, int bx, double **c, int **q, double **dq, d
     dct_forward(j->dct, x, c);
     const double var = calculate_block_variance(x, 8);
     quantize(j->qc, c, q, var);
-    dequantize(j->qc, q, dq, var);
-    dct_inverse(j->dct, dq, rec);
+    if (!j->forward_only) {
+        dequantize(j->qc, q, dq, var);
+        dct_inverse(j->dct, dq, rec);
+    }
     const long b = (long)by * (j->width / 8) + bx;
     for (int i = 0; i < 8; ++i)
         for (int k = 0; k < 8; ++k) {
@@ -91,12 +95,13 @@ static void *worker(void *arg) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 9) {
-        fprintf(stderr, "usage: %s pixels width height quality adaptive threads reps out\n", argv[0]);
+    if (argc != 9 && argc != 10) {
+        fprintf(stderr, "usage: %s pixels width height quality adaptive threads reps out [forward]\n", argv[0]);
         return 2;
     }
     const int w = atoi(argv[2]), h = atoi(argv[3]), quality = atoi(argv[4]), adaptive = atoi(argv[5]);
     const int threads = atoi(argv[6]), reps = atoi(argv[7]);
+    const int forward_only = argc == 10 && strcmp(argv[9], "forward") == 0;
     if (w <= 0 || h <= 0 || w % 8 || h % 8 || threads < 1 || threads > 64 || reps < 1) return 2;
     unsigned char *px = malloc((size_t)w * h);
     FILE *f = fopen(argv[1], "rb");
@@ -118,7 +123,7 @@ int main(int argc, char **argv) {
     pthread_t th[64];
     Job jobs[64];
     for (int t = 0; t < threads; ++t) {
-        jobs[t] = (Job){px, w, h, threads, reps, t, dct, qc, q_out, r_out, &bar};
+        jobs[t] = (Job){px, w, h, threads, reps, t, forward_only, dct, qc, q_out, r_out, &bar};
         pthread_create(&th[t], NULL, worker, &jobs[t]);
     }
     pthread_barrier_wait(&bar); /* every worker has made its first calls */
@@ -147,7 +152,7 @@ int main(int argc, char **argv) {
     printf("blocks:%ld\n", nblk * reps);
     printf("seconds:%.6f\n", el);
     printf("pipelines_per_s:%.1f\n", nblk * reps / el);
-    printf("calls_per_s:%.1f\n", 5.0 * nblk * reps / el);
+    printf("calls_per_s:%.1f\n", (forward_only ? 3.0 : 5.0) * nblk * reps / el);
     printf("rand_draws:%ld\n", draws);
     printf("rand_ok:%d\n", bad == 0);
     dct_free(dct);
