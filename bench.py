@@ -321,7 +321,7 @@ def cpu_model() -> str:
 
 def gpu_identity():
     """The box's GPU as rocm-smi reports it (serial, HBM vendor, memory/compute partition):
-    boxes of this pool differ by up to ~15 % on the same bytes, and the
+    boxes of this pool differ by up to ~15 % on the same bytes (HISTORY.md 3.1b), and the
     bench's own ceilings are the normaliser; this says which box a line came from."""
     import re
     import shutil
@@ -835,7 +835,7 @@ def timed_steady(fn, steps, dev, prewarm_ms=LEG_PREWARM_MS):
     """Wall time of `steps` back-to-back calls of a secondary leg's step, measured
     the way the headline is (main()): the step first runs back to back, untimed,
     for about `prewarm_ms` -- between legs the GPU idles while the host works, and
-    an idle MI355X drops its clocks within milliseconds -- then the
+    an idle MI355X drops its clocks within milliseconds (HISTORY.md 3.1b) -- then the
     timed steps are bracketed by a barrier and a synchronize on both sides; the
     max over ranks.  The pre-warm is a COUNT of calls that every rank agrees on
     (one timed call, the max over ranks of the count it suggests): a step may hold
@@ -1012,7 +1012,7 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
                     forward runs, and twice it),
                     reading THE SAME PIXEL BYTES (the luma and chroma stacks back to
                     back): HBM moves constant data faster than random data (up to
-                    9 %), so a ceiling over a constant buffer is not a
+                    9 %, HISTORY.md 3.1b), so a ceiling over a constant buffer is not a
                     ceiling of this workload -- flat_1to2_nt_nt_const shows that
                     effect and is not a candidate ceiling;
       read_only, write_only(_nt) : dctq_diag_stream 2/3/4 over the same byte counts;

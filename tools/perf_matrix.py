@@ -3,7 +3,7 @@ multi-plane launch) for every input kind x plan, each next to the no-arithmetic
 movement of the same planes (dctq_diag_movement_planes) on the same box.  The
 forward runs through the product library (libdct_amd.so), the movement through
 the diagnostic one (round 4: through the diagnostic library the tie-heavy rows
-read 5-8 % slower):
+read 5-8 % slower, HISTORY.md 8.5):
 HIP events, medians of samples of 3 launches back to back after one untimed
 launch of the same kind (steady state: profiles/r02/policy_b2b.md).  Prints one
 line per configuration.

@@ -1,6 +1,6 @@
 """Same-box A/B of the fused round trip (BASELINE configs[4]) on the bench step:
 64 4K 4:2:0 frames (Y stack + Cb/Cr stack), q50, interleaved rounds, each sample
-3 launches back to back after one untimed launch (steady state).
+3 launches back to back after one untimed launch (steady state, HISTORY.md 3.1b).
 
     python tools/rt_ab.py [--rounds 10] [--kind uniform] [--quality 50] [--adaptive 0] [ENTRY...]
 

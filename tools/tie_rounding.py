@@ -3,7 +3,7 @@ For (u, v) in {0, 4}^2 the exact coefficient of an integer block is a multiple o
 1 block in 8 is an exact half-integer; the reference's fp64 sum (src/dct.c:57-74, D from
 dct_init's expression, src/dct.c:19-30) lands slightly above, below or exactly on it.
 Counts over random blocks show the direction is ~evenly split, i.e. there is no cheaper
-rule than the reference-order evaluation itself (DESIGN.md 3.2, round 4 session 3).
+rule than the reference-order evaluation itself (HISTORY.md 3.2, round 4 session 3).
 
     python tools/tie_rounding.py [blocks_per_coefficient]"""
 import math
