@@ -6,7 +6,8 @@
 
 ENTRY: "fused" (the product library), "fused64" (the diagnostic library with the
 paired fp64 inverse forced), "flat" (dctq_diag_stream kind 5: the same bytes as a
-flat 1:2:4 stream), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
+flat 1:2:4 stream over a constant source), "flatpx" (the same over the workload's own pixel
+bytes: HBM moves constant data faster), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
 "fused:PATH" (those of a build at PATH, tools/ubench/variant.sh, DIAG=1 for mv).
 Default: fused fused64 flat mv.
 """
@@ -44,7 +45,8 @@ stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 cp = C.cast((C.c_void_p * 2)(*[t.data_ptr() for t in co]), C.c_void_p)
 rp = C.cast((C.c_void_p * 2)(*[t.data_ptr() for t in rec]), C.c_void_p)
 nflat = nblk // 64 * 64
-src = torch.full((nflat * 64,), 7, dtype=torch.uint8, device="cuda")
+src = torch.full((nflat * 64,), 7, dtype=torch.uint8, device="cuda")  # "flat": a constant source (rounds 3-5)
+srcpx = torch.cat([p.reshape(-1) for p in planes])[:nflat * 64].contiguous()  # "flatpx": the workload's pixels
 dst = torch.empty(nflat * 384, dtype=torch.uint8, device="cuda")
 
 
@@ -62,9 +64,10 @@ def lib_plan(path, inverse=None):
 runs = {}
 for e in args.entries:
     kind, _, path = e.partition(":")
-    if kind == "flat":
+    if kind in ("flat", "flatpx"):
         D = dct_amd.diag()
-        runs[e] = lambda D=D: D.dctq_diag_stream(5, src.data_ptr(), dst.data_ptr(), nflat, stream)
+        buf = src if kind == "flat" else srcpx
+        runs[e] = lambda D=D, buf=buf: D.dctq_diag_stream(5, buf.data_ptr(), dst.data_ptr(), nflat, stream)
         continue
     if kind in ("fused", "fused64"):
         L, h = lib_plan(path or (dct_amd.LIB_PATH if kind == "fused" else dct_amd.DIAG_PATH),
@@ -94,7 +97,7 @@ for r in range(args.rounds + 1):
 # differs from the fp32 one within its bound)
 first = None
 for k, fn in runs.items():
-    if k == "flat":
+    if k in ("flat", "flatpx"):
         continue
     assert fn() == 0, k
     torch.cuda.synchronize()
