@@ -73,6 +73,7 @@ def _bind(L: C.CDLL, diagnostic: bool) -> C.CDLL:
             "dctq_diag_plan_set_inverse": ([vp, i], i),
             "dctq_debug_inverse_bound": ([i, i, C.POINTER(i)], C.c_double),
             "dctq_debug_symbol_bytes": ([i, i], i),
+            "dctq_diag_legacy_lanes": ([C.POINTER(i), C.POINTER(i)], i),
             "dctq_diag_movement_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_movement_v2_planes": ([vp, C.POINTER(_Plane), i, vp, vp], i),
             "dctq_diag_movement_grid_planes": ([vp, C.POINTER(_Plane), i, vp, i, vp], i),

@@ -98,6 +98,10 @@ int dctq_debug_fastdiv(uint32_t d, uint32_t n);
 double dctq_debug_inverse_bound(int quality, int adaptive, int *admitted);
 /* The encoder's symbol bytes (2 or 4) for a standard-table plan (dctq_plan_symbol_bytes). */
 int dctq_debug_symbol_bytes(int quality, int adaptive);
+/* The legacy per-block API's lanes (legacy.hip: a stream + staging buffer per host
+ * thread and device): how many were ever created, and how many wait in the pool for
+ * a new thread (their threads exited).  For calls made through this library. */
+int dctq_diag_legacy_lanes(int *made, int *pooled);
 
 #ifdef __cplusplus
 }

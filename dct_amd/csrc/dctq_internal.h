@@ -55,6 +55,8 @@ class LaunchIsolation {
 bool runtime_started();
 void note_runtime_started();
 void forget_stream(const void *stream);
+// legacy.hip: per-thread lanes of the per-block API created so far / pooled (diagnostics)
+void legacy_lane_counts(int *made, int *pooled);
 
 
 // Resident workgroups per CU of `kernel` at `threads` per workgroup (>= 1).  The

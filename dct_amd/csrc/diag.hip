@@ -116,6 +116,12 @@ double dctq_debug_inverse_bound(int quality, int adaptive, int *admitted) {
     return b;
 }
 
+int dctq_diag_legacy_lanes(int *made, int *pooled) {
+    if (!made || !pooled) return dctq::fail(DCTQ_EINVAL, "NULL pointer");
+    dctq::legacy_lane_counts(made, pooled);
+    return DCTQ_OK;
+}
+
 int dctq_debug_symbol_bytes(int quality, int adaptive) {
     (void)adaptive;  // adaptive divisors Q (2 - nv) >= Q: the same bound
     dctq::DevTables t;

@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <optional>
 #include <vector>
@@ -205,7 +206,8 @@ struct Lane {
 __global__ void k_nop() {}
 
 std::mutex g_pool_mu;
-std::vector<Lane *> g_pool;  // lanes of threads that have exited
+std::vector<Lane *> g_pool;        // lanes of threads that have exited
+std::atomic<int> g_lanes_made{0};  // lanes ever created (diagnostics: dctq_diag_legacy_lanes)
 
 struct ThreadLanes {
     std::vector<Lane *> lanes;
@@ -240,6 +242,7 @@ Lane &lane() {
     if (!l) {
         l = new Lane();
         l->device = d;
+        g_lanes_made.fetch_add(1, std::memory_order_relaxed);
         LCHK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking), "hipStreamCreateWithFlags(legacy lane)");
         (void)l->stage(kStageMin);
         hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, l->stream);  // the stream's first queue, under isolation
@@ -335,6 +338,15 @@ void elementwise(int mode, int n, double **m, int flag, double variance, const d
 }
 
 }  // namespace
+
+// Lanes created so far and lanes waiting in the pool (threads that exited), for the
+// diagnostic library's dctq_diag_legacy_lanes (tests: a host that keeps spawning
+// threads holds at most as many lanes as it had threads alive at once).
+void dctq::legacy_lane_counts(int *made, int *pooled) {
+    *made = g_lanes_made.load(std::memory_order_relaxed);
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    *pooled = (int)g_pool.size();
+}
 
 extern "C" {
 

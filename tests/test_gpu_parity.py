@@ -1317,6 +1317,76 @@ def test_legacy_transforms_bit_exact(L, blocks):
         L.dct_free(ctx)
 
 
+def test_legacy_thread_churn(T, dm):
+    """The per-block API from threads that come and go (legacy.hip lanes): 4 rounds of 6 concurrent
+    Python threads (each an OS thread; ctypes drops the GIL inside the calls), each running
+    dct_forward -> calculate_block_variance -> quantize on its own blocks over ONE shared context,
+    n = 8 (zero-copy staging) and n = 40 (device scratch).  Every result equals the oracle's, and
+    the lanes are reused: a thread that exits returns its lane to the pool, so 24 threads over 4
+    rounds create at most 6 lanes (+ this thread's), with the rest pooled at the end.  Calls go
+    through the diagnostic library, which exports the same API and counts its lanes."""
+    import threading
+    import oracle as O
+    lib = dm.diag()
+    P2 = C.POINTER(C.POINTER(C.c_double))
+    I2 = C.POINTER(C.POINTER(C.c_int))
+    lib.dct_init.restype = C.POINTER(DCTContext)
+    lib.dct_forward.argtypes = [C.POINTER(DCTContext), P2, P2]
+    lib.alloc_array.restype = P2
+    lib.alloc_int_array.restype = I2
+    lib.free_array.argtypes = [P2, C.c_int]
+    lib.free_int_array.argtypes = [I2, C.c_int]
+    lib.quant_init.restype = C.POINTER(QuantContext)
+    lib.quantize.argtypes = [C.POINTER(QuantContext), P2, I2, C.c_double]
+    lib.calculate_block_variance.argtypes = [P2, C.c_int]
+    lib.calculate_block_variance.restype = C.c_double
+    made0, pooled0 = C.c_int(), C.c_int()
+    dm._check(lib.dctq_diag_legacy_lanes(C.byref(made0), C.byref(pooled0)), lib)
+    ctxs = {n: (lib.dct_init(n), lib.quant_init(n, 75, 1)) for n in (8, 40)}
+    rng = np.random.default_rng(606)
+    errs = []
+
+    def work(seed):
+        try:
+            r = np.random.default_rng(seed)
+            for n in (8, 40, 8):
+                dct, qc = ctxs[n]
+                x = r.integers(-128, 128, (n, n)).astype(np.float64)
+                a, c, q = _put(lib, x), lib.alloc_array(n, n), lib.alloc_int_array(n, n)
+                lib.dct_forward(dct, a, c)
+                var = lib.calculate_block_variance(a, n)
+                lib.quantize(qc, c, q, var)
+                want_c = O.forward(x)
+                assert (_get(c, n).view(np.uint64) == want_c.view(np.uint64)).all(), (seed, n)
+                assert var == O.variance(x), (seed, n)
+                assert np.array_equal(_get_i(q, n), O.quantize(want_c, 75, 1, O.variance(x))), (seed, n)
+                lib.free_array(a, n)
+                lib.free_array(c, n)
+                lib.free_int_array(q, n)
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+
+    import time
+    made, pooled = C.c_int(), C.c_int()
+    for rnd in range(4):
+        th = [threading.Thread(target=work, args=(int(rng.integers(1 << 30)),)) for _ in range(6)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs, errs
+        # Python's join returns before the OS thread has run its thread_local destructors (which
+        # hand the lanes back): wait for them before the next round starts its threads
+        t_end = time.time() + 10
+        while True:
+            dm._check(lib.dctq_diag_legacy_lanes(C.byref(made), C.byref(pooled)), lib)
+            if pooled.value >= pooled0.value + 6 or time.time() > t_end:
+                break
+            time.sleep(0.01)
+    assert made.value - made0.value <= 6, (made0.value, made.value)
+    assert pooled.value == pooled0.value + 6 and pooled.value <= made.value, (pooled0.value, pooled.value, made.value)
+
+
 def test_legacy_large_blocks_and_variance(L):
     """The per-block API on both sides of the legacy kernels' staging switch (4 n^2 doubles up to 32 KiB:
     one workgroup with D, T and the block in LDS over the zero-copy buffer; above: device scratch and one
