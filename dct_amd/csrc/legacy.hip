@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <optional>
 #include <vector>
@@ -57,6 +58,20 @@ __device__ __forceinline__ double dot_ordered(const double *x, const double *y, 
     return acc;
 }
 
+// One-workgroup kernels end by writing `seq` to the calling lane's done flag in
+// pinned host memory, after every output of the workgroup has reached the host
+// (each thread's system-scope fence, then the barrier): the calling thread spins
+// on that flag instead of a stream synchronize (finish()).  The flag address goes
+// through a VGPR so the store is a vector store.
+__device__ __forceinline__ void signal_done(uint32_t *done, uint32_t seq) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        asm volatile("" : "+v"(done));
+        __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // Small blocks (4 n^2 doubles <= kLdsBytes: n <= 32, the codec's n = 8): ONE
 // workgroup per call, its D, T and input staged in LDS from the pinned zero-copy
 // buffer in one parallel round trip over the host link, the result written
@@ -64,7 +79,8 @@ __device__ __forceinline__ double dot_ordered(const double *x, const double *y, 
 constexpr int kLdsBytes = 32 * 1024;
 template <bool FWD>
 __global__ void k_transform_small(int n, const double *__restrict__ dh, const double *__restrict__ th,
-                                  const double *__restrict__ inh, double *__restrict__ out) {
+                                  const double *__restrict__ inh, double *__restrict__ out, uint32_t *done,
+                                  uint32_t seq) {
     extern __shared__ double lds[];
     const int nn = n * n;
     double *d = lds, *t = lds + nn, *in = lds + 2 * nn, *tmp = lds + 3 * nn;
@@ -79,6 +95,7 @@ __global__ void k_transform_small(int n, const double *__restrict__ dh, const do
     __syncthreads();
     for (int e = threadIdx.x; e < nn; e += blockDim.x)
         out[e] = FWD ? dot_ordered(d, tmp, n, e / n, e % n) : dot_ordered(tmp, d, n, e / n, e % n);
+    signal_done(done, seq);
 }
 
 // Any n (the reference takes any block size, src/dct.c:7-40): the packed
@@ -101,11 +118,10 @@ __device__ double adjusted(const double *src, int e, double variance, int is_qua
 
 // src/quantization.c:113-131 (mode 0), :133-151 (mode 1), :171-211 (mode 2),
 // src/dct.c:123-129 (mode 3: (int) round(c)).
-__global__ void k_elementwise(int mode, int nn, const double *__restrict__ m, int adaptive, double variance,
-                              const double *__restrict__ din, const int *__restrict__ iin, double *__restrict__ dout,
-                              int *__restrict__ iout) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= nn) return;
+__device__ __forceinline__ void elementwise_one(int mode, int e, const double *__restrict__ m, int adaptive,
+                                                double variance, const double *__restrict__ din,
+                                                const int *__restrict__ iin, double *__restrict__ dout,
+                                                int *__restrict__ iout) {
     switch (mode) {
     case 0: {
         const double mm = adaptive ? adjusted(m, e, variance, 1) : m[e];
@@ -124,22 +140,33 @@ __global__ void k_elementwise(int mode, int nn, const double *__restrict__ m, in
     }
 }
 
+__global__ void k_elementwise(int mode, int nn, const double *__restrict__ m, int adaptive, double variance,
+                              const double *__restrict__ din, const int *__restrict__ iin, double *__restrict__ dout,
+                              int *__restrict__ iout, uint32_t *done, uint32_t seq) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < nn) elementwise_one(mode, e, m, adaptive, variance, din, iin, dout, iout);
+    if (done) signal_done(done, seq);  // one-workgroup launches only (n <= 16)
+}
+
 // src/quantization.c:153-169 -- sequential row-major sums (order matters for
 // non-integer input), one thread; small blocks first copied from the zero-copy
 // buffer into LDS by the whole workgroup (one parallel round trip over the
 // host link), large ones read from device scratch.
-__global__ void k_variance_small(int nn, const double *__restrict__ xh, double *__restrict__ out) {
+__global__ void k_variance_small(int nn, const double *__restrict__ xh, double *__restrict__ out, uint32_t *done,
+                                 uint32_t seq) {
     extern __shared__ double x[];
     for (int e = threadIdx.x; e < nn; e += blockDim.x) x[e] = xh[e];
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    double s = 0.0, s2 = 0.0;
-    for (int k = 0; k < nn; ++k) {
-        s += x[k];
-        s2 += x[k] * x[k];
+    if (threadIdx.x == 0) {
+        double s = 0.0, s2 = 0.0;
+        for (int k = 0; k < nn; ++k) {
+            s += x[k];
+            s2 += x[k] * x[k];
+        }
+        const double mean = s / nn;
+        out[0] = (s2 / nn) - (mean * mean);
     }
-    const double mean = s / nn;
-    out[0] = (s2 / nn) - (mean * mean);
+    signal_done(done, seq);
 }
 
 __global__ void k_variance(int nn, const double *__restrict__ x, double *__restrict__ out) {
@@ -159,8 +186,9 @@ __global__ void k_variance(int nn, const double *__restrict__ x, double *__restr
 // thread gets one LANE per device: its own non-blocking stream, a pinned,
 // device-mapped staging buffer (zero-copy: a call packs its row-pointer arrays
 // into it, the kernel reads its inputs from it and writes its outputs back into
-// it over the host link, and the call synchronizes its own stream -- no memcpy
-// calls) and, for large blocks, a device scratch buffer.  No lock is held in
+// it over the host link -- no memcpy calls), a done flag in pinned coherent host
+// memory (finish_signalled) and, for large blocks, a device scratch buffer.  No
+// lock is held in
 // steady state: only a thread's FIRST call on a device (it creates the lane's
 // stream and launches on it first, which is where libhsa may call srand/rand)
 // and a buffer's growth (a HIP allocation) take the rand isolation lock
@@ -179,13 +207,19 @@ struct Lane {
     size_t host_bytes = 0;
     unsigned char *scratch = nullptr;
     size_t scratch_bytes = 0;
+    uint32_t *done_host = nullptr;  // the one-workgroup kernels' completion flag (signal_done)
+    uint32_t *done_dev = nullptr;
+    uint32_t seq = 0;               // the value the next call's kernel writes there
+    uint32_t since_sync = 0;        // calls since the lane's stream was last synchronized
     unsigned char *stage(size_t need) {
         if (need > host_bytes) {
             DCTQ_ENTRY;  // an allocation: may reach the runtime's rand()
             if (host) (void)hipHostFree(host);
             host = nullptr;
             const size_t bytes = need > kStageMin ? need : kStageMin;
-            LCHK(hipHostMalloc((void **)&host, bytes, hipHostMallocMapped), "hipHostMalloc(legacy staging)");
+            // coherent: the kernel's outputs reach host memory before its done flag does
+            LCHK(hipHostMalloc((void **)&host, bytes, hipHostMallocMapped | hipHostMallocCoherent),
+                 "hipHostMalloc(legacy staging)");
             LCHK(hipHostGetDevicePointer((void **)&hdev, host, 0), "hipHostGetDevicePointer");
             host_bytes = bytes;
         }
@@ -245,6 +279,10 @@ Lane &lane() {
         g_lanes_made.fetch_add(1, std::memory_order_relaxed);
         LCHK(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking), "hipStreamCreateWithFlags(legacy lane)");
         (void)l->stage(kStageMin);
+        LCHK(hipHostMalloc((void **)&l->done_host, 64, hipHostMallocMapped | hipHostMallocCoherent),
+             "hipHostMalloc(legacy done flag)");
+        LCHK(hipHostGetDevicePointer((void **)&l->done_dev, l->done_host, 0), "hipHostGetDevicePointer");
+        __atomic_store_n(l->done_host, 0u, __ATOMIC_RELEASE);
         hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, l->stream);  // the stream's first queue, under isolation
         LCHK(hipGetLastError(), "legacy lane launch");
         LCHK(hipStreamSynchronize(l->stream), "hipStreamSynchronize");
@@ -256,6 +294,30 @@ Lane &lane() {
 void finish(const Lane &ln, const char *what) {
     LCHK(hipGetLastError(), what);
     LCHK(hipStreamSynchronize(ln.stream), "hipStreamSynchronize");
+}
+
+// The call's one-workgroup kernel writes ln.seq to the done flag after its outputs
+// (signal_done): the calling thread spins on the flag over the host link instead of
+// a stream synchronize.  Fallbacks: past 50 ms of spinning (a slow device, or a
+// launch that failed without an error code) the stream is synchronized and the flag
+// must then be there; and every 1024 calls the stream is synchronized anyway, so the
+// runtime retires the lane's launches.
+void finish_signalled(Lane &ln, const char *what) {
+    LCHK(hipGetLastError(), what);
+    const uint32_t want = ln.seq;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; __atomic_load_n(ln.done_host, __ATOMIC_ACQUIRE) != want; ++i) {
+        if ((i & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) {
+            LCHK(hipStreamSynchronize(ln.stream), "hipStreamSynchronize");
+            if (__atomic_load_n(ln.done_host, __ATOMIC_ACQUIRE) != want) die("legacy kernel finished without signalling");
+            break;
+        }
+        __builtin_ia32_pause();
+    }
+    if (++ln.since_sync >= 1024u) {
+        ln.since_sync = 0;
+        LCHK(hipStreamSynchronize(ln.stream), "hipStreamSynchronize");
+    }
 }
 
 void pack(double **a, int n, double *dst) {
@@ -284,11 +346,11 @@ void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
         const size_t lds = sizeof(double) * 4 * nn;
         if (fwd)
             hipLaunchKernelGGL(k_transform_small<true>, dim3(1), dim3(threads), lds, ln.stream, n, dv, dv + nn,
-                               dv + 2 * nn, (double *)dv + 3 * nn);
+                               dv + 2 * nn, (double *)dv + 3 * nn, ln.done_dev, ++ln.seq);
         else
             hipLaunchKernelGGL(k_transform_small<false>, dim3(1), dim3(threads), lds, ln.stream, n, dv, dv + nn,
-                               dv + 2 * nn, (double *)dv + 3 * nn);
-        finish(ln, "transform launch");
+                               dv + 2 * nn, (double *)dv + 3 * nn, ln.done_dev, ++ln.seq);
+        finish_signalled(ln, "transform launch");
         unpack(h + 3 * nn, n, output);
         return;
     }
@@ -330,9 +392,14 @@ void elementwise(int mode, int n, double **m, int flag, double variance, const d
     if (iin) memcpy(hi, iin, sizeof(int) * nn);
     double *dm = (double *)ln.hdev, *dd = dm + nn, *ddo = dd + nn;
     int *di = (int *)(ddo + nn), *dio = di + nn;
-    hipLaunchKernelGGL(k_elementwise, dim3((nn + 255) / 256), dim3(256), 0, ln.stream, mode, nn, dm, flag, variance,
-                       dd, di, ddo, dio);
-    finish(ln, "elementwise launch");
+    const unsigned grid = (unsigned)((nn + 255) / 256);
+    const bool one = grid == 1;  // n <= 16: one workgroup, which signals its own completion
+    hipLaunchKernelGGL(k_elementwise, dim3(grid), dim3(256), 0, ln.stream, mode, nn, dm, flag, variance, dd, di, ddo,
+                       dio, one ? ln.done_dev : nullptr, one ? ++ln.seq : 0u);
+    if (one)
+        finish_signalled(ln, "elementwise launch");
+    else
+        finish(ln, "elementwise launch");
     if (dout) memcpy(dout, (double *)h + 2 * nn, sizeof(double) * nn);
     if (iout) memcpy(iout, (int *)((double *)h + 3 * nn) + nn, sizeof(int) * nn);
 }
@@ -498,8 +565,8 @@ double calculate_block_variance(double **block, int block_size) {
         pack(block, block_size, hs);
         const int threads = nn < 256 ? (int)((nn + 63) / 64) * 64 : 256;
         hipLaunchKernelGGL(k_variance_small, dim3(1), dim3(threads), sizeof(double) * nn, ln.stream, (int)nn, dv,
-                           dv + nn);
-        finish(ln, "variance launch");
+                           dv + nn, ln.done_dev, ++ln.seq);
+        finish_signalled(ln, "variance launch");
         return hs[nn];
     }
     std::vector<double> h(nn + 1);
