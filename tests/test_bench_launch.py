@@ -204,3 +204,36 @@ def test_legs_watchdog_prints_the_line():
     d = json.loads(lines[0])
     assert d["value"] == 5.0 and d["fine"] == 1 and d["legs"]["fine"]["ok"] is True, d
     assert "deadline" in d["legs"]["stuck"]["error"], d
+
+
+def test_merge_methods_and_fault_injection():
+    """bench.merge_methods joins a gather leg's all-gather and p2p halves (which run as separate,
+    fail-soft legs): flags hold over the methods that ran, a missing half carries its leg status,
+    and the gathered tensors are compared when both ran.  inject_p2p_fault touches only the last
+    rank's p2p leg."""
+    import types
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    full = torch.arange(12, dtype=torch.int16).reshape(3, 4)
+    a = {"methods": {"all_gather": {"gathered_equals_unsharded": True}}, "gathered_equals_unsharded": True,
+         "own_slice_intact": True, "methods_gather_the_same": True, "_full": full}
+    p = {"methods": {"p2p": {"gathered_equals_unsharded": False}}, "gathered_equals_unsharded": False,
+         "own_slice_intact": True, "methods_gather_the_same": True, "_full": full.clone()}
+    m = bench.merge_methods(a, p, "p2p", None)
+    assert set(m["methods"]) == {"all_gather", "p2p"} and "_full" not in m
+    assert m["gathered_equals_unsharded"] is False and m["own_slice_intact"] is True
+    assert m["methods_gather_the_same"] is True
+    p2 = dict(p, _full=full + 1)
+    assert bench.merge_methods(a, p2, "p2p", None)["methods_gather_the_same"] is False
+    st = {"error": "TimeoutError: gloo recv"}
+    m = bench.merge_methods(a, None, "p2p", st)
+    assert m["methods"]["p2p"] == st and m["gathered_equals_unsharded"] is True and m["methods_gather_the_same"] is None
+    assert bench.merge_methods(None, None, "p2p", st) is None
+    assert bench.merge_methods(None, p, "p2p", None)["methods"] == p["methods"]
+    args = types.SimpleNamespace(gather_fault="p2p-raise", dist_timeout=1.0)
+    bench.inject_p2p_fault(args, 4, 2, "p2p")  # not the last rank
+    bench.inject_p2p_fault(args, 4, 3, "all_gather")  # not the p2p leg
+    with pytest.raises(RuntimeError, match="injected"):
+        bench.inject_p2p_fault(args, 4, 3, "p2p")
+    bench.inject_p2p_fault(types.SimpleNamespace(gather_fault="offset", dist_timeout=1.0), 4, 3, "p2p")
