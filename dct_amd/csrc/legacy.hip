@@ -78,10 +78,8 @@ __device__ __forceinline__ void signal_done(uint32_t *done, uint32_t seq) {
 // straight back to it.
 constexpr int kLdsBytes = 32 * 1024;
 template <bool FWD>
-__global__ void k_transform_small(int n, const double *__restrict__ dh, const double *__restrict__ th,
-                                  const double *__restrict__ inh, double *__restrict__ out, uint32_t *done,
-                                  uint32_t seq) {
-    extern __shared__ double lds[];
+__device__ __forceinline__ void transform_body(int n, const double *__restrict__ dh, const double *__restrict__ th,
+                                               const double *__restrict__ inh, double *__restrict__ out, double *lds) {
     const int nn = n * n;
     double *d = lds, *t = lds + nn, *in = lds + 2 * nn, *tmp = lds + 3 * nn;
     for (int e = threadIdx.x; e < nn; e += blockDim.x) {
@@ -95,6 +93,31 @@ __global__ void k_transform_small(int n, const double *__restrict__ dh, const do
     __syncthreads();
     for (int e = threadIdx.x; e < nn; e += blockDim.x)
         out[e] = FWD ? dot_ordered(d, tmp, n, e / n, e % n) : dot_ordered(tmp, d, n, e / n, e % n);
+}
+
+template <bool FWD>
+__global__ void k_transform_small(int n, const double *__restrict__ dh, const double *__restrict__ th,
+                                  const double *__restrict__ inh, double *__restrict__ out, uint32_t *done,
+                                  uint32_t seq) {
+    extern __shared__ double lds[];
+    transform_body<FWD>(n, dh, th, inh, out, lds);
+    signal_done(done, seq);
+}
+
+// n == 8, the codec's block (round 6): the 64-value inputs travel as kernel
+// arguments, which the runtime writes into device memory with the dispatch, so the
+// kernel reads them without a round trip over the host link; only the outputs and
+// the done flag cross it (posted writes).
+struct Vals64 {
+    double v[64];
+};
+struct Ints64 {
+    int v[64];
+};
+template <bool FWD>
+__global__ void k_transform8(Vals64 d, Vals64 t, Vals64 in, double *__restrict__ out, uint32_t *done, uint32_t seq) {
+    __shared__ double lds[4 * 64];
+    transform_body<FWD>(8, d.v, t.v, in.v, out, lds);
     signal_done(done, seq);
 }
 
@@ -148,13 +171,18 @@ __global__ void k_elementwise(int mode, int nn, const double *__restrict__ m, in
     if (done) signal_done(done, seq);  // one-workgroup launches only (n <= 16)
 }
 
+__global__ void k_elementwise8(int mode, int adaptive, double variance, Vals64 m, Vals64 din, Ints64 iin,
+                               double *__restrict__ dout, int *__restrict__ iout, uint32_t *done, uint32_t seq) {
+    if (threadIdx.x < 64) elementwise_one(mode, threadIdx.x, m.v, adaptive, variance, din.v, iin.v, dout, iout);
+    signal_done(done, seq);
+}
+
 // src/quantization.c:153-169 -- sequential row-major sums (order matters for
 // non-integer input), one thread; small blocks first copied from the zero-copy
 // buffer into LDS by the whole workgroup (one parallel round trip over the
 // host link), large ones read from device scratch.
-__global__ void k_variance_small(int nn, const double *__restrict__ xh, double *__restrict__ out, uint32_t *done,
-                                 uint32_t seq) {
-    extern __shared__ double x[];
+__device__ __forceinline__ void variance_body(int nn, const double *__restrict__ xh, double *__restrict__ out,
+                                              double *x) {
     for (int e = threadIdx.x; e < nn; e += blockDim.x) x[e] = xh[e];
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -166,6 +194,18 @@ __global__ void k_variance_small(int nn, const double *__restrict__ xh, double *
         const double mean = s / nn;
         out[0] = (s2 / nn) - (mean * mean);
     }
+}
+
+__global__ void k_variance_small(int nn, const double *__restrict__ xh, double *__restrict__ out, uint32_t *done,
+                                 uint32_t seq) {
+    extern __shared__ double x[];
+    variance_body(nn, xh, out, x);
+    signal_done(done, seq);
+}
+
+__global__ void k_variance8(Vals64 xv, double *__restrict__ out, uint32_t *done, uint32_t seq) {
+    __shared__ double x[64];
+    variance_body(64, xv.v, out, x);
     signal_done(done, seq);
 }
 
@@ -336,6 +376,22 @@ void transform(DCTContext *ctx, double **input, double **output, bool fwd) {
     check_n(n);
     const size_t nn = (size_t)n * n;
     Lane &ln = lane();
+    if (n == 8) {
+        Vals64 d, t, in;
+        pack(ctx->dct_matrix, 8, d.v);
+        pack(ctx->transposed_dct, 8, t.v);
+        pack(input, 8, in.v);
+        double *h = (double *)ln.stage(sizeof(double) * 64);
+        if (fwd)
+            hipLaunchKernelGGL(k_transform8<true>, dim3(1), dim3(64), 0, ln.stream, d, t, in, (double *)ln.hdev,
+                               ln.done_dev, ++ln.seq);
+        else
+            hipLaunchKernelGGL(k_transform8<false>, dim3(1), dim3(64), 0, ln.stream, d, t, in, (double *)ln.hdev,
+                               ln.done_dev, ++ln.seq);
+        finish_signalled(ln, "transform launch");
+        unpack(h, 8, output);
+        return;
+    }
     if (4 * nn * sizeof(double) <= (size_t)kLdsBytes) {
         double *h = (double *)ln.stage(sizeof(double) * 4 * nn);
         const double *dv = (const double *)ln.hdev;
@@ -384,6 +440,22 @@ void elementwise(int mode, int n, double **m, int flag, double variance, const d
     const int nn = n * n;
     const size_t bytes = sizeof(double) * 3 * (size_t)nn + sizeof(int) * 2 * (size_t)nn;
     Lane &ln = lane();
+    if (n == 8) {
+        Vals64 mv, dv{};
+        Ints64 iv{};
+        pack(m, 8, mv.v);
+        if (din) memcpy(dv.v, din, sizeof dv.v);
+        if (iin) memcpy(iv.v, iin, sizeof iv.v);
+        unsigned char *h = ln.stage(sizeof(double) * 64 + sizeof(int) * 64);
+        double *ddo = (double *)ln.hdev;
+        int *dio = (int *)(ddo + 64);
+        hipLaunchKernelGGL(k_elementwise8, dim3(1), dim3(64), 0, ln.stream, mode, flag, variance, mv, dv, iv, ddo, dio,
+                           ln.done_dev, ++ln.seq);
+        finish_signalled(ln, "elementwise launch");
+        if (dout) memcpy(dout, h, sizeof(double) * 64);
+        if (iout) memcpy(iout, h + sizeof(double) * 64, sizeof(int) * 64);
+        return;
+    }
     unsigned char *h = ln.stage(bytes);
     double *hm = (double *)h, *hd = hm + nn;
     int *hi = (int *)(hd + 2 * nn);
@@ -559,6 +631,14 @@ double calculate_block_variance(double **block, int block_size) {
     check_n(block_size);
     const size_t nn = (size_t)block_size * block_size;
     Lane &ln = lane();
+    if (block_size == 8) {
+        Vals64 xv;
+        pack(block, 8, xv.v);
+        double *hs = (double *)ln.stage(sizeof(double));
+        hipLaunchKernelGGL(k_variance8, dim3(1), dim3(64), 0, ln.stream, xv, (double *)ln.hdev, ln.done_dev, ++ln.seq);
+        finish_signalled(ln, "variance launch");
+        return hs[0];
+    }
     if (nn * sizeof(double) <= (size_t)kLdsBytes) {
         double *hs = (double *)ln.stage(sizeof(double) * (nn + 1));
         double *dv = (double *)ln.hdev;
