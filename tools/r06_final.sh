@@ -30,6 +30,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_rt -o run --output
   python tools/rt_bench.py 64 > $O/rt_bench.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_aux -o run --output-format csv -- \
   python tools/aux_bench.py > $O/aux_bench.log 2>&1 &&
-echo "collected" &&
-timeout -k 10 300 python -u tools/rt_ab.py --rounds 10 fused flat flatpx mv > $O/rt_flat_src_ab.log 2>&1 &&
-echo "ab ok"
+echo "collected"
