@@ -70,9 +70,14 @@ int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes
  *   kind 5: the round trip's mix, flat: 64 B read : 128 + 256 B written per
  *           block (per wave 4 x 1 KiB loads, 24 x 1 KiB nt stores), persistent;
  *   kind 6, 7: kind 0 on a grid of 16 x / 32 x the resident one (the forward's
- *           grid and twice it), capped at one 64-block batch per wave.
- * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kind 5: blocks * 384),
- * both 16-byte aligned. */
+ *           grid and twice it), capped at one 64-block batch per wave;
+ *   kind 8: kind 5's bytes in the round trip's output layout: each batch's 8 KiB
+ *           to region A (the first blocks * 128 bytes of dst: the coefficients)
+ *           and 16 KiB to region B (the rest: the recon);
+ *   kind 9: kind 8 with the stores in the round trip's three 8 KiB groups and a
+ *           vmcnt(0) drain before each of the last two.
+ * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kinds 5, 8, 9: blocks *
+ * 384), both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
 
 /* The v2 queue kernel (variant 4) keeps a tie-path pixel stash per (device,

@@ -53,6 +53,40 @@ __global__ __launch_bounds__(256) void stream124(const u4v *__restrict__ src, ch
     }
 }
 
+// The flat 1:2:4 stream in the fused round trip's OUTPUT layout (round 6): the 8 KiB of a batch's
+// coefficients go to region A (dst[8 KiB * b]) and its 16 KiB of recon to region B (dst[8 KiB * nb
+// + 16 KiB * b]), two separate arrays as the API has them.  GROUPS: the stores leave in the round
+// trip's three 8 KiB groups with a vmcnt(0) drain before each of the last two (its LDS read-backs).
+template <bool GROUPS>
+__global__ __launch_bounds__(256) void stream124_split(const u4v *__restrict__ src, char *__restrict__ dst,
+                                                       uint32_t nb) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < nb; b += gridDim.x * 4) {
+        u4v v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(src + (size_t)b * 256 + k * 64 + lane);
+        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 8192, 0, 8192, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rb =
+            __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)nb * 8192 + (size_t)b * 16384, 0, 16384, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+                __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)m, 0, 0, 0}, ra, lane * 16,
+                                                       (k * 2 + m) * 1024, 2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (GROUPS) __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), as before the round trip's read-backs
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+                    __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)(2 + 2 * h + m), 0, 0, 0}, rb,
+                                                           lane * 16, (h * 8 + k * 2 + m) * 1024, 2);
+        }
+    }
+}
+
 // read-only: 4 x 16 B per thread, xor-reduced (the store never happens)
 __global__ __launch_bounds__(256) void stream_read(const u4v *__restrict__ src, u4v *__restrict__ sink, size_t n16) {
     const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
@@ -220,7 +254,9 @@ int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, voi
         hipLaunchKernelGGL(stream12<2>, dim3(g < want ? g : want), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb);
         break;
     }
-    default: return fail(DCTQ_EINVAL, "kind must be 0..7");
+    case 8: hipLaunchKernelGGL(stream124_split<false>, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
+    case 9: hipLaunchKernelGGL(stream124_split<true>, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
+    default: return fail(DCTQ_EINVAL, "kind must be 0..9");
     }
     HIPCHK(hipGetLastError(), "diag stream launch");
     return DCTQ_OK;

@@ -7,7 +7,9 @@
 ENTRY: "fused" (the product library), "fused64" (the diagnostic library with the
 paired fp64 inverse forced), "flat" (dctq_diag_stream kind 5: the same bytes as a
 flat 1:2:4 stream over a constant source), "flatpx" (the same over the workload's own pixel
-bytes: HBM moves constant data faster), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
+bytes: HBM moves constant data faster), "flat2" (the same bytes, pixel source, in the round trip's
+two-array output layout: coefficients and recon in separate regions), "flat2g" (flat2 with the round
+trip's three store groups and their drains), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
 "fused:PATH" (those of a build at PATH, tools/ubench/variant.sh, DIAG=1 for mv).
 Default: fused fused64 flat mv.
 """
@@ -64,10 +66,11 @@ def lib_plan(path, inverse=None):
 runs = {}
 for e in args.entries:
     kind, _, path = e.partition(":")
-    if kind in ("flat", "flatpx"):
+    if kind in ("flat", "flatpx", "flat2", "flat2g"):
         D = dct_amd.diag()
         buf = src if kind == "flat" else srcpx
-        runs[e] = lambda D=D, buf=buf: D.dctq_diag_stream(5, buf.data_ptr(), dst.data_ptr(), nflat, stream)
+        sk = {"flat": 5, "flatpx": 5, "flat2": 8, "flat2g": 9}[kind]
+        runs[e] = lambda D=D, buf=buf, sk=sk: D.dctq_diag_stream(sk, buf.data_ptr(), dst.data_ptr(), nflat, stream)
         continue
     if kind in ("fused", "fused64"):
         L, h = lib_plan(path or (dct_amd.LIB_PATH if kind == "fused" else dct_amd.DIAG_PATH),
@@ -97,7 +100,7 @@ for r in range(args.rounds + 1):
 # differs from the fp32 one within its bound)
 first = None
 for k, fn in runs.items():
-    if k in ("flat", "flatpx"):
+    if k.startswith("flat"):
         continue
     assert fn() == 0, k
     torch.cuda.synchronize()
