@@ -954,7 +954,14 @@ def rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev, b2b=3):
       flat_124 : dctq_diag_stream 5 -- the same byte counts as a flat persistent
                  stream (1 KiB loads, 24 x 1 KiB nt stores per 64 blocks) over the
                  workload's own pixel bytes (flat_124_const: over a constant buffer,
-                 as rounds 3-5 measured it).
+                 as rounds 3-5 measured it);
+      plane_124: dctq_diag_stream 11 -- flat_124's stores (the round trip's two output
+                 arrays, three drained groups) with the round trip's READ shape: each
+                 lane loads its block's 8 rows (8 B each) from a 3840-px-wide plane.
+                 Same box, same bytes: the plane's row pitch alone costs ~4 % against
+                 flat_124 (profiles/r06/INDEX.md, rt_read_shape_ab), so this, not the
+                 flat stream, is the no-arithmetic ceiling of a block transform over
+                 image planes.
     fused_over_own_movement is the kernel's time against its own data movement.
     Overwrites co/rec (run after the parity copies)."""
     import statistics
@@ -971,16 +978,17 @@ def rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev, b2b=3):
     dst = torch.empty(nflat * 384, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
 
-    def flat(buf):
-        rc = D.dctq_diag_stream(5, buf.data_ptr(), dst.data_ptr(), nflat, stream)
+    def flat(buf, kind=5):
+        rc = D.dctq_diag_stream(kind, buf.data_ptr(), dst.data_ptr(), nflat, stream)
         if rc:
-            raise RuntimeError(f"dctq_diag_stream(5) rc={rc}")
+            raise RuntimeError(f"dctq_diag_stream({kind}) rc={rc}")
 
     bpb = 64 + 128 + 256
     cases = {"fused": (lambda: plan.round_trip_planes(pls, outs=co, recons=rec), nblk * bpb),
              "movement": (lambda: dplan.diag_rt_movement_planes(pls, co, rec), nblk * bpb),
              "flat_124": (lambda: flat(src), nflat * bpb),
-             "flat_124_const": (lambda: flat(src7), nflat * bpb)}
+             "flat_124_const": (lambda: flat(src7), nflat * bpb),
+             "plane_124": (lambda: flat(src, 11), nflat * bpb)}
     times = {k: [] for k in cases}
     for r in range(args.ceiling_rounds + 1):
         for k, (fn, _) in cases.items():
@@ -997,7 +1005,8 @@ def rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev, b2b=3):
     frac = {k: cases[k][1] / med[k] / 1e9 / HBM_PEAK_GBS for k in cases}
     del src, src7, dst
     return {"fused_frac": frac["fused"], "movement_frac": frac["movement"], "flat_124_frac": frac["flat_124"],
-            "flat_124_const_frac": frac["flat_124_const"],
+            "flat_124_const_frac": frac["flat_124_const"], "plane_124_frac": frac["plane_124"],
+            "fused_over_plane_124": frac["fused"] / frac["plane_124"],
             "fused_over_own_movement": frac["fused"] / frac["movement"],
             "fused_over_flat_124": frac["fused"] / frac["flat_124"],
             "fused_over_flat_124_const": frac["fused"] / frac["flat_124_const"], "rounds": args.ceiling_rounds,
@@ -1026,6 +1035,12 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
                     9 %, HISTORY.md 3.1b), so a ceiling over a constant buffer is not a
                     ceiling of this workload -- flat_1to2_nt_nt_const shows that
                     effect and is not a candidate ceiling;
+      plane_1to2_x32 : dctq_diag_stream 14 -- flat_1to2_nt_nt_x32's stores with the
+                    forward's READ shape (each lane its block's 8 rows, 8 B each, from
+                    a 3840-px-wide plane): the no-arithmetic ceiling of a block
+                    transform over image planes, reported as forward_over_plane_1to2
+                    (not a candidate for `pattern`: it is a model of the workload's
+                    reads, profiles/r06/INDEX.md rt_read_shape_ab);
       read_only, write_only(_nt) : dctq_diag_stream 2/3/4 over the same byte counts;
       phased_*    : a read-only launch then a write-only launch, timed as a pair,
                     i.e. the 1:2 traffic with no mix (not reachable by one launch
@@ -1065,6 +1080,7 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
         "flat_1to2_nt_nt_x16": (lambda: diag_stream(6), nflat * BYTES_PER_BLOCK),
         "flat_1to2_nt_nt_x32": (lambda: diag_stream(7), nflat * BYTES_PER_BLOCK),
         "flat_1to2_nt_nt_const": (lambda: diag_stream(0, buf=src7), nflat * BYTES_PER_BLOCK),
+        "plane_1to2_x32": (lambda: diag_stream(14), nflat * BYTES_PER_BLOCK),
         "flat_1to2_nt_plain": (lambda: diag_stream(1), nflat * BYTES_PER_BLOCK),
         "read_only": (lambda: diag_stream(2), nflat * 64),
         "write_only": (lambda: diag_stream(3), nflat * 128),
@@ -1091,7 +1107,8 @@ def ceilings_leg(args, plan, luma, chroma, coef_y, coef_c, dev, rounds=10, b2b=3
     del src, src7, dst
     return {"pattern": best, "achieved": frac[best] * HBM_PEAK_GBS, "frac": frac[best],
             "forward_frac": frac["forward"], "forward_over_ceiling": frac["forward"] / frac[best],
-            "forward_over_own_movement": frac["forward"] / frac["movement_v3"], "rounds": rounds,
+            "forward_over_own_movement": frac["forward"] / frac["movement_v3"],
+            "forward_over_plane_1to2": frac["forward"] / frac["plane_1to2_x32"], "rounds": rounds,
             "launches_per_sample": b2b,
             "hw_ceilings": {k: {"median_us": med[k] * 1e6, "frac": frac[k],
                                 **({"note": "two kernels: an upper bound no single launch that transforms the "

@@ -75,8 +75,18 @@ int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes
  *           to region A (the first blocks * 128 bytes of dst: the coefficients)
  *           and 16 KiB to region B (the rest: the recon);
  *   kind 9: kind 8 with the stores in the round trip's three 8 KiB groups and a
- *           vmcnt(0) drain before each of the last two.
- * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kinds 5, 8, 9: blocks *
+ *           vmcnt(0) drain before each of the last two;
+ *   kind 10: kind 9 with the round trip's load shape: each lane loads its block's
+ *           8 rows as 8-byte nt buffer loads, the batch's 4 KiB contiguous;
+ *   kind 11: kind 10 over a 3840-px-wide plane (480 blocks per block row: the
+ *           luma plane's row pitch between a block's rows);
+ *   kind 12, 13: kind 11 with workgroup-contiguous / wave-contiguous runs of
+ *           batches instead of the grid-stride order;
+ *   kind 14: kind 7 with the forward's load shape over a 3840-px-wide plane (each
+ *           lane its block's 8 rows, 8 B each);
+ *   kind 15: kind 11 with 16-byte loads (per instruction, rows 2k and 2k + 1 of the
+ *           batch, two blocks' row slices per lane).
+ * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kinds 5, 8-13: blocks *
  * 384), both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
 

@@ -14,6 +14,7 @@ namespace dctq {
 namespace {
 
 typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u2v2 __attribute__((ext_vector_type(2)));
 
 // Flat 1:2 stream (profiles/r02/hbm_ceilings.md "s12"): wave-batch b reads
 // src[4 KiB * b, +4 KiB) with 4 x 16-B-per-lane loads and writes
@@ -83,6 +84,124 @@ __global__ __launch_bounds__(256) void stream124_split(const u4v *__restrict__ s
                 for (int m = 0; m < 2; ++m)
                     __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)(2 + 2 * h + m), 0, 0, 0}, rb,
                                                            lane * 16, (h * 8 + k * 2 + m) * 1024, 2);
+        }
+    }
+}
+
+// stream124_split<true> with the round trip's READ shape: each lane loads its block's
+// 8 pixel rows as 8-byte non-temporal buffer loads.  W = 0: the 64 blocks of a batch
+// are contiguous 512-B row slices (lane-contiguous, only the load width differs from
+// kind 9); W = 3840: blocks of a 3840-px-wide plane (480 blocks per block row, a batch
+// may straddle two block rows), the luma plane's pattern.  Blocks past the last whole
+// block row wrap to the start (same bytes moved).
+// MAP: which batches a wave takes.  0: grid-stride (batch blockIdx * 4 + wave, then
+// + grid * 4: the product kernels' order); 1: workgroup-contiguous (workgroup i
+// sweeps batches [i K, (i + 1) K) with its 4 waves side by side); 2: wave-contiguous
+// (each wave sweeps its own run of consecutive batches).
+template <int W, int MAP = 0>
+__global__ __launch_bounds__(256) void stream124_rows(const uint8_t *__restrict__ src, char *__restrict__ dst,
+                                                      uint32_t nb) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src), (short)0, (int)(nb * 4096u), 0x00020000);
+    constexpr uint32_t kBpr = W ? W / 8 : 64;  // blocks per block row
+    const uint32_t nfull = W ? nb * 64u / kBpr * kBpr : nb * 64u;
+    const uint32_t nwg = gridDim.x, kwg = (nb + nwg - 1) / nwg, kw = (nb + nwg * 4 - 1) / (nwg * 4);
+    const uint32_t b0 = MAP == 0 ? blockIdx.x * 4 + wv : MAP == 1 ? blockIdx.x * kwg + wv : (blockIdx.x * 4 + wv) * kw;
+    const uint32_t b1 = MAP == 0 ? nb : MAP == 1 ? min(nb, (blockIdx.x + 1) * kwg) : min(nb, b0 + kw);
+    const uint32_t bs = MAP == 0 ? nwg * 4 : MAP == 1 ? 4u : 1u;
+    for (uint32_t b = b0; b < b1; b += bs) {
+        const uint32_t n = (b * 64u + (uint32_t)lane) % nfull;
+        const uint32_t off = W ? (n / kBpr) * 8u * W + (n % kBpr) * 8u : (n >> 6) * 4096u + (n & 63u) * 8u;
+        const uint32_t st = W ? (uint32_t)W : 512u;
+        u2v2 r[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) r[y] = __builtin_amdgcn_raw_buffer_load_b64(rs, off + y * st, 0, 2);
+        u4v v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = u4v{r[2 * k].x, r[2 * k].y, r[2 * k + 1].x, r[2 * k + 1].y};
+        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 8192, 0, 8192, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rb =
+            __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)nb * 8192 + (size_t)b * 16384, 0, 16384, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+                __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)m, 0, 0, 0}, ra, lane * 16,
+                                                       (k * 2 + m) * 1024, 2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+                    __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)(2 + 2 * h + m), 0, 0, 0}, rb,
+                                                           lane * 16, (h * 8 + k * 2 + m) * 1024, 2);
+        }
+    }
+}
+
+// Kind 11 with 16-byte loads: per instruction k the wave reads rows 2k (lanes 0-31) and
+// 2k + 1 (lanes 32-63) of the batch's 64 blocks, two blocks' row slices per lane (4 loads
+// per batch instead of 8; a lane-per-block kernel would need a cross-lane exchange after).
+__global__ __launch_bounds__(256) void stream124_rows16(const uint8_t *__restrict__ src, char *__restrict__ dst,
+                                                        uint32_t nb) {
+    constexpr uint32_t kW = 3840, kBpr = kW / 8;
+    const int lane = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src), (short)0, (int)(nb * 4096u), 0x00020000);
+    const uint32_t nfull = nb * 64u / kBpr * kBpr;
+    for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < nb; b += gridDim.x * 4) {
+        const uint32_t n = (b * 64u + 2u * (uint32_t)(lane & 31)) % nfull;
+        const uint32_t off = (n / kBpr) * 8u * kW + (n % kBpr) * 8u + (uint32_t)(lane >> 5) * kW;
+        u4v v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 2 * k * kW, 0, 2);
+        const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 8192, 0, 8192, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rb =
+            __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)nb * 8192 + (size_t)b * 16384, 0, 16384, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int m = 0; m < 2; ++m)
+                __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)m, 0, 0, 0}, ra, lane * 16,
+                                                       (k * 2 + m) * 1024, 2);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int m = 0; m < 2; ++m)
+                    __builtin_amdgcn_raw_buffer_store_b128(v[k] ^ u4v{(unsigned)(2 + 2 * h + m), 0, 0, 0}, rb,
+                                                           lane * 16, (h * 8 + k * 2 + m) * 1024, 2);
+        }
+    }
+}
+
+// Kind 7 (the flat 1:2 stream on a 32x grid, one batch per wave) with the forward's READ
+// shape: each lane loads its block's 8 rows as 8-byte non-temporal buffer loads from a
+// 3840-px-wide plane (480 blocks per block row; blocks past the last whole block row wrap).
+__global__ __launch_bounds__(256) void stream12_plane(const uint8_t *__restrict__ src, char *__restrict__ dst,
+                                                      uint32_t nb) {
+    constexpr uint32_t kW = 3840, kBpr = kW / 8;
+    const int lane = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src), (short)0, (int)(nb * 4096u), 0x00020000);
+    const uint32_t nfull = nb * 64u / kBpr * kBpr;
+    for (uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6); b < nb; b += gridDim.x * 4) {
+        const uint32_t n = (b * 64u + (uint32_t)lane) % nfull;
+        const uint32_t off = (n / kBpr) * 8u * kW + (n % kBpr) * 8u;
+        u2v2 r[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) r[y] = __builtin_amdgcn_raw_buffer_load_b64(rs, off + y * kW, 0, 2);
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(dst + (size_t)b * 8192, 0, 8192, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u4v v = u4v{r[2 * k].x, r[2 * k].y, r[2 * k + 1].x, r[2 * k + 1].y};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rc, lane * 16, k * 1024, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(v ^ u4v{1, 0, 0, 0}, rc, lane * 16, (k + 4) * 1024, 2);
         }
     }
 }
@@ -256,7 +375,17 @@ int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, voi
     }
     case 8: hipLaunchKernelGGL(stream124_split<false>, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
     case 9: hipLaunchKernelGGL(stream124_split<true>, dim3(grid), dim3(256), 0, s, (const u4v *)src, (char *)dst, nb); break;
-    default: return fail(DCTQ_EINVAL, "kind must be 0..9");
+    case 10: hipLaunchKernelGGL(stream124_rows<0>, dim3(grid), dim3(256), 0, s, (const uint8_t *)src, (char *)dst, nb); break;
+    case 11: hipLaunchKernelGGL(stream124_rows<3840>, dim3(grid), dim3(256), 0, s, (const uint8_t *)src, (char *)dst, nb); break;
+    case 12: hipLaunchKernelGGL((stream124_rows<3840, 1>), dim3(grid), dim3(256), 0, s, (const uint8_t *)src, (char *)dst, nb); break;
+    case 13: hipLaunchKernelGGL((stream124_rows<3840, 2>), dim3(grid), dim3(256), 0, s, (const uint8_t *)src, (char *)dst, nb); break;
+    case 14: {
+        const unsigned want = (nb + 3) / 4, g = (unsigned)grid * 32u;
+        hipLaunchKernelGGL(stream12_plane, dim3(g < want ? g : want), dim3(256), 0, s, (const uint8_t *)src, (char *)dst, nb);
+        break;
+    }
+    case 15: hipLaunchKernelGGL(stream124_rows16, dim3(grid), dim3(256), 0, s, (const uint8_t *)src, (char *)dst, nb); break;
+    default: return fail(DCTQ_EINVAL, "kind must be 0..15");
     }
     HIPCHK(hipGetLastError(), "diag stream launch");
     return DCTQ_OK;

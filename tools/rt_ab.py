@@ -9,7 +9,10 @@ paired fp64 inverse forced), "flat" (dctq_diag_stream kind 5: the same bytes as 
 flat 1:2:4 stream over a constant source), "flatpx" (the same over the workload's own pixel
 bytes: HBM moves constant data faster), "flat2" (the same bytes, pixel source, in the round trip's
 two-array output layout: coefficients and recon in separate regions), "flat2g" (flat2 with the round
-trip's three store groups and their drains), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
+trip's three store groups and their drains), "rows8" (flat2g with the round trip's load shape: 8-byte row
+loads per lane, the batch contiguous), "rows2d" (rows8 over a 3840-px-wide plane: the luma row pitch), "rows2d_wg" / "rows2d_wave" (rows2d
+with workgroup- / wave-contiguous runs of batches), "rows2d16" (rows2d with 16-byte loads, two rows per
+instruction), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
 "fused:PATH" (those of a build at PATH, tools/ubench/variant.sh, DIAG=1 for mv).
 Default: fused fused64 flat mv.
 """
@@ -66,10 +69,10 @@ def lib_plan(path, inverse=None):
 runs = {}
 for e in args.entries:
     kind, _, path = e.partition(":")
-    if kind in ("flat", "flatpx", "flat2", "flat2g"):
+    if kind in ("flat", "flatpx", "flat2", "flat2g", "rows8", "rows2d", "rows2d_wg", "rows2d_wave", "rows2d16"):
         D = dct_amd.diag()
         buf = src if kind == "flat" else srcpx
-        sk = {"flat": 5, "flatpx": 5, "flat2": 8, "flat2g": 9}[kind]
+        sk = {"flat": 5, "flatpx": 5, "flat2": 8, "flat2g": 9, "rows8": 10, "rows2d": 11, "rows2d_wg": 12, "rows2d_wave": 13, "rows2d16": 15}[kind]
         runs[e] = lambda D=D, buf=buf, sk=sk: D.dctq_diag_stream(sk, buf.data_ptr(), dst.data_ptr(), nflat, stream)
         continue
     if kind in ("fused", "fused64"):
@@ -100,7 +103,7 @@ for r in range(args.rounds + 1):
 # differs from the fp32 one within its bound)
 first = None
 for k, fn in runs.items():
-    if k.startswith("flat"):
+    if k.startswith(("flat", "rows")):
         continue
     assert fn() == 0, k
     torch.cuda.synchronize()
