@@ -240,14 +240,13 @@ __device__ __forceinline__ void tile_dma(const int16_t *coef, long long t, long 
     }
 }
 
-// Each path re-reads the tile row itself, so nothing but scalars is live across
-// the path choice and each path gets its own register allocation (a shared
-// 32-register row made the compiler hold 188-336 VGPRs).
+// Every path works on the row classify() read (d: the lane's 64 coefficients as 32
+// dwords), so the tile is read out of LDS once per tile (round 6: -2 to -3 % on
+// uniform input against a re-read per path, profiles/r06/huf_keep_row_ab; the row
+// live across the path choice costs the dense path a few spilled loop invariants).
 template <int N, bool FWD = false, typename NextTile>
 __device__ __forceinline__ void sparse_runs(char *mine, const Hist &h, int lane, uint32_t &nodes, uint32_t &lmax,
-                                            NextTile next_tile) {
-    uint32_t d[32];
-    tile_row<FWD>(mine, lane, d);
+                                            NextTile next_tile, const uint32_t (&d)[32]) {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): every lane has its row before the columns overwrite the tile
     __builtin_amdgcn_wave_barrier();
     // branch-free compaction: every value is written at the next slot, which advances
@@ -299,16 +298,12 @@ __device__ __forceinline__ void sparse_runs(char *mine, const Hist &h, int lane,
 
 template <bool FWD = false, typename NextTile>
 __device__ __forceinline__ void dense_runs(char *mine, const Hist &h, int lane, uint32_t &nodes, uint32_t &lmax,
-                                           NextTile next_tile) {
+                                           NextTile next_tile, const uint32_t (&d)[32]) {
     uint32_t a[64];
-    {
-        uint32_t d[32];
-        tile_row<FWD>(mine, lane, d);
 #pragma unroll
-        for (int h = 0; h < 32; ++h) {
-            a[2 * h] = (d[h] << 16) - 1u;
-            a[2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
-        }
+    for (int h = 0; h < 32; ++h) {
+        a[2 * h] = (d[h] << 16) - 1u;
+        a[2 * h + 1] = (d[h] & 0xFFFF0000u) - 1u;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the row is in registers, the stage is free
     __builtin_amdgcn_wave_barrier();
@@ -342,11 +337,10 @@ struct NarrowLeaves {
     uint32_t hrows;      // wave-uniform: 16 + kHeavyRows when heavy[] was read, else 16
 };
 
-template <bool FWD = false, typename NextTile>
-__device__ __forceinline__ void narrow_leaves(const char *mine, char *ctr, int lane, int wv, int32_t vmin,
-                                              uint32_t span, bool last_zero, NextTile next_tile, NarrowLeaves &L) {
-    uint32_t d[32];
-    tile_row<FWD>(mine, lane, d);
+template <typename NextTile>
+__device__ __forceinline__ void narrow_leaves(char *ctr, int lane, int wv, int32_t vmin, uint32_t span,
+                                              bool last_zero, NextTile next_tile, NarrowLeaves &L,
+                                              const uint32_t (&d)[32]) {
     // the row is in registers and the stage is free: the next tile streams in meanwhile
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     next_tile();
@@ -557,14 +551,13 @@ struct TileClass {
 };
 
 template <bool FWD = false>
-__device__ __forceinline__ TileClass classify(const char *mine, int lane, int nb) {
+__device__ __forceinline__ TileClass classify(const char *mine, int lane, int nb, uint32_t (&d)[32]) {
     TileClass c;
     c.nz = 0;
     c.narrow = false;
     c.vmin = 0;
     c.span = 64;
     {
-        uint32_t d[32];
         tile_row<FWD>(mine, lane, d);
         c.last_zero = (d[31] >> 16) == 0u;
         // Nonzeros of dwords [k0, k1): unsigned min(h, 1) is 1 for any nonzero half;
@@ -615,8 +608,8 @@ __device__ __forceinline__ TileClass classify(const char *mine, int lane, int nb
             if (!looks_dense && __builtin_amdgcn_ballot_w64(c.nz > 32)) span_test();  // dense after all
         }
     }
-    // the paths re-read the row: a memory clobber keeps the compiler from reusing
-    // (and holding) these 32 registers across the choice
+    // the row stays in d for the paths; the compiler barrier keeps the paths' LDS
+    // writes (compacted keys, counters) after these reads, as in the measured build
     asm volatile("" ::: "memory");
     return c;
 }
@@ -628,7 +621,7 @@ __device__ __forceinline__ TileClass classify(const char *mine, int lane, int nb
 // bit counts.
 template <bool FWD = false, typename NextTile>
 __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int lane, int wv, int nb,
-                                                   const TileClass &cl, NextTile next_tile) {
+                                                   const TileClass &cl, NextTile next_tile, const uint32_t (&d)[32]) {
     const Hist h{ctr, (uint32_t)(lane * 4), 8u * (uint32_t)wv};
     const uint32_t nz = cl.nz;
     const bool last_zero = cl.last_zero;
@@ -639,11 +632,11 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int la
     const bool lane_merge = dense;  // the dense paths merge per lane (occupancy mask)
     uint32_t wpl = 0, pending = 0;
     if (!__builtin_amdgcn_ballot_w64(nz > 16))
-        sparse_runs<16, FWD>(mine, h, lane, nodes, lmax, next_tile);
+        sparse_runs<16, FWD>(mine, h, lane, nodes, lmax, next_tile, d);
     else if (!__builtin_amdgcn_ballot_w64(nz > 32))
-        sparse_runs<32, FWD>(mine, h, lane, nodes, lmax, next_tile);
+        sparse_runs<32, FWD>(mine, h, lane, nodes, lmax, next_tile, d);
     else
-        dense_runs<FWD>(mine, h, lane, nodes, lmax, next_tile);
+        dense_runs<FWD>(mine, h, lane, nodes, lmax, next_tile, d);
     if (last_zero) h.add(1, 1);
     // ---- bucket merge (see the header): wpl = sum of internal node weights.  Lanes
     // past the tail hold one leaf (the zero block's last 0) and run as any other,
@@ -730,13 +723,14 @@ __device__ __forceinline__ uint32_t sort_tile_bits(char *mine, char *ctr, int la
 // overwritten (the next tile's DMA, or nothing).
 template <bool FWD = false, typename NextTile>
 __device__ __forceinline__ uint32_t tile_bits(char *mine, char *ctr, int lane, int wv, int nb, NextTile next_tile) {
-    const TileClass cl = classify<FWD>(mine, lane, nb);
+    uint32_t row[32];
+    const TileClass cl = classify<FWD>(mine, lane, nb, row);
     if (cl.narrow) {
         NarrowLeaves L;
-        narrow_leaves<FWD>(mine, ctr, lane, wv, cl.vmin, cl.span, cl.last_zero, next_tile, L);  // the zero leaf included
+        narrow_leaves(ctr, lane, wv, cl.vmin, cl.span, cl.last_zero, next_tile, L, row);  // the zero leaf included
         return 8u * L.count + narrow_merge(L, wv);
     }
-    return sort_tile_bits<FWD>(mine, ctr, lane, wv, nb, cl, next_tile);
+    return sort_tile_bits<FWD>(mine, ctr, lane, wv, nb, cl, next_tile, row);
 }
 
 // The tie passes of huffman_from_pixels: passes of <= 8 entries run 8 lanes per entry

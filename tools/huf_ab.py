@@ -3,7 +3,10 @@ builds (tools/ubench/libvar_*.so; libvar_no*.so are ablations whose output is no
 checked), same quantized planes (64 4K luma frames of
 each input kind, q50), interleaved, HIP events; outputs must match.
 
-    python tools/huf_ab.py [frames]
+    python tools/huf_ab.py [frames] [--pixels]
+
+--pixels: dctq_huffman_bits_planes (forward + quantization + sizes in one launch,
+huffman_from_pixels_kernel) over the same luma frames instead.
 """
 import ctypes as C
 import glob
@@ -18,16 +21,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import dct_amd  # noqa: E402
 
-F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+PIXELS = "--pixels" in sys.argv
+argv = [a for a in sys.argv[1:] if a != "--pixels"]
+F = int(argv[0]) if argv else 64
 nblk = F * 480 * 270
 libs = {"default": dct_amd.lib()}
 for p in sorted(glob.glob(os.path.join(ROOT, "tools", "ubench", "libvar_*.so"))):
     L = C.CDLL(p)
     L.dctq_huffman_bits.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_void_p]
     libs[os.path.basename(p)[7:-3]] = L
+plans = {}
+for k, L in libs.items():
+    L.dctq_plan_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    h = C.c_void_p()
+    assert L.dctq_plan_create(50, 0, C.byref(h)) == 0
+    L.dctq_huffman_bits_planes.argtypes = [C.c_void_p, C.POINTER(dct_amd._Plane), C.c_int, C.c_void_p, C.c_void_p]
+    plans[k] = h
 s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
 for kind in ("uniform", "smooth", "const", "extreme"):
-    coef = dct_amd.Plan(50, 0).forward_quant(dct_amd.synth(9, kind, 3840, 2160, F))
+    px = dct_amd.synth(9, kind, 3840, 2160, F)
+    desc = dct_amd.plane_desc(px)
+    coef = dct_amd.Plan(50, 0).forward_quant(px)
     out = torch.zeros(nblk, dtype=torch.int32, device="cuda")  # shared by every build (see tools/rle_ab.py)
     ref = None
     times = {k: [] for k in libs}
@@ -39,7 +53,10 @@ for kind in ("uniform", "smooth", "const", "extreme"):
     for r in range(9):
         for k, L in libs.items():
             # steady state: one untimed launch, then 3 back to back (the bench's method)
-            launch = lambda: L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(out.data_ptr()), s)
+            if PIXELS:
+                launch = lambda: L.dctq_huffman_bits_planes(plans[k], C.byref(desc), 1, C.c_void_p(out.data_ptr()), s)
+            else:
+                launch = lambda: L.dctq_huffman_bits(C.c_void_p(coef.data_ptr()), nblk, C.c_void_p(out.data_ptr()), s)
             assert launch() == 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
