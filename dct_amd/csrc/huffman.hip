@@ -375,15 +375,18 @@ __device__ __forceinline__ void narrow_leaves(char *ctr, int lane, int wv, int32
     // counts (q50 noise: 32-40 of 64): the first nck wave-uniform chunks of 8 rows
     // (span conditions are monotone in the chunk).  Rows of skipped chunks are
     // never read, so nothing is materialised for them.
+    // (4-row chunks: 3.5 % slower on uniform input, 16-row chunks the same as 8:
+    // profiles/r06/huf_keep_row_ab/chunk_*.log)
+    constexpr int CH = 8, NCH = 64 / CH;
     int nck = 1;
 #pragma unroll
-    for (int c8 = 1; c8 < 8; ++c8) nck += __builtin_amdgcn_ballot_w64(span > (uint32_t)(8 * c8)) != 0 ? 1 : 0;
+    for (int c8 = 1; c8 < NCH; ++c8) nck += __builtin_amdgcn_ballot_w64(span > (uint32_t)(CH * c8)) != 0 ? 1 : 0;
     uint32_t raw[64];
 #pragma unroll
-    for (int c8 = 0; c8 < 8; ++c8) {
+    for (int c8 = 0; c8 < NCH; ++c8) {
         if (c8 < nck) {
 #pragma unroll
-            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) raw[s_] = take_raw((uint32_t)s_);
+            for (int s_ = CH * c8; s_ < CH * c8 + CH; ++s_) raw[s_] = take_raw((uint32_t)s_);
         }
     }
     // A counter is kept as its leaf's address: one v_perm moves the wave's byte of
@@ -392,10 +395,10 @@ __device__ __forceinline__ void narrow_leaves(char *ctr, int lane, int wv, int32
     const uint32_t leaf_sel = 0x0C0C0000u | ((4u + (uint32_t)wv) << 8);
     uint32_t amax = base;
 #pragma unroll
-    for (int c8 = 0; c8 < 8; ++c8) {
+    for (int c8 = 0; c8 < NCH; ++c8) {
         if (c8 < nck) {
 #pragma unroll
-            for (int s_ = 8 * c8; s_ < 8 * c8 + 8; ++s_) {
+            for (int s_ = CH * c8; s_ < CH * c8 + CH; ++s_) {
                 const uint32_t a = __builtin_amdgcn_perm(raw[s_], base, leaf_sel);
                 amax = a > amax ? a : amax;
                 __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(ctr + a), inc, __ATOMIC_RELAXED,
