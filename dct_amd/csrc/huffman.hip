@@ -363,6 +363,8 @@ __device__ __forceinline__ void narrow_leaves(char *ctr, int lane, int wv, int32
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
     // zeros: their count gives the symbol count; then only c[63] == 0 leaves one
+    // (reading this counter first in the read-out batch instead, without a round trip
+    // of its own, measured within noise: profiles/r06/huf_keep_row_ab/zero_in_batch_*.log)
     uint32_t zeros = 0;
     if (vmin <= 0 && vmin > -64) {
         const uint32_t z = (uint32_t)(-vmin);
