@@ -4,8 +4,13 @@
 // Why no single-pass (decoupled look-back) scan: it needs tiles claimed in
 // order from one atomic word, and one word saturates near 88 claims/us on
 // MI355X (MI355X_MICROARCH.md "dequeue"), while the count pass streams ~700
-// 64-block tiles/us.  The counts therefore go reduce-then-scan: per-tile
-// totals, one workgroup scan of the totals, a fix-up.
+// 64-block tiles/us.  A static grid-stride assignment (no claim word, the grid
+// co-resident) fails the other way: the batches of one sweep are all in flight
+// together, so a wave's predecessors have only their aggregates, and its
+// look-back walks back through up to one sweep (~4 096 batches, 64 per flag
+// read at ~1 us each) per batch, against ~6 us of work per batch.  The counts
+// therefore go reduce-then-scan: per-tile totals, one workgroup scan of the
+// totals, a fix-up.
 #pragma once
 #include "dctq_internal.h"
 
