@@ -783,7 +783,8 @@ def test_diag_stream_moves_bytes(T, dm):
     """The hardware-ceiling streams of the diagnostic library (bench.py
     roofline.movement_ceiling) move what they claim: the flat 1:2 stream writes
     each 1 KiB input chunk twice (the second copy with bit 0 of its first dword
-    flipped), the write-only stream covers the whole output."""
+    flipped), the write-only stream covers the whole output; the round trip's 1:2:4
+    streams (kinds 5, 8-13, 15) and the plane-read 1:2 stream (14) run and write."""
     D = dm.diag()
     n = 64 * 40
     src = T.randint(0, 256, (n * 64,), dtype=T.uint8, device="cuda")
@@ -805,7 +806,25 @@ def test_diag_stream_moves_bytes(T, dm):
         T.cuda.synchronize()
         w = dst.view(-1, 16).cpu().numpy().view(np.uint32)
         assert (w[:, 2] == 7).all() and (w[:, 3] == 9).all()
-    assert D.dctq_diag_stream(9, src.data_ptr(), dst.data_ptr(), n, s) != 0
+    # the round trip's streams (1:2:4 bytes): the same bytes in the two-array layout with
+    # and without the drained store groups; the plane-read streams in any batch order
+    out = {}
+    for kind in (5, 8, 9, 10, 11, 12, 13, 15):
+        dst = T.zeros(n * 384, dtype=T.uint8, device="cuda")
+        assert D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), n, s) == 0, kind
+        T.cuda.synchronize()
+        out[kind] = dst.cpu().numpy()
+        assert out[kind].any(), kind
+    assert np.array_equal(out[8], out[9])
+    assert np.array_equal(out[11], out[12]) and np.array_equal(out[11], out[13])
+    a = src.view(-1, 4, 1024).cpu().numpy()  # kind 8: region A holds each batch's 4 KiB twice (bit 0 of dword 0 flipped)
+    ra = out[8][:n * 128].reshape(-1, 8, 1024)
+    assert np.array_equal(ra[:, 0::2], a)
+    dst = T.zeros(n * 128, dtype=T.uint8, device="cuda")
+    assert D.dctq_diag_stream(14, src.data_ptr(), dst.data_ptr(), n, s) == 0
+    T.cuda.synchronize()
+    assert dst.cpu().numpy().any()
+    assert D.dctq_diag_stream(16, src.data_ptr(), dst.data_ptr(), n, s) != 0
 
 
 def _sym32(sym):
