@@ -328,7 +328,9 @@ __device__ __forceinline__ void dense_runs(char *mine, const Hist &h, int lane, 
 // and runs the register merge).  A software-pipelined kernel loop that merged one
 // tile while the next tile's LDS phases were in flight measured no faster
 // (profiles/r03/huffman_restructure_ab.log).
-constexpr int kHeavyRows = 4;  // weight rows 17.. read back without waiting (q50 noise: largest leaf ~20)
+// weight rows 17.. read back without waiting (q50 noise: largest leaf ~20; 6 or 8 rows measured the
+// same or slower, profiles/r06/huf_keep_row_ab/heavy_rows_*.log)
+constexpr int kHeavyRows = 4;
 struct NarrowLeaves {
     uint32_t light[16];  // weight rows 1..16 as read (the wave's byte at 8 * wave)
     uint32_t heavy[kHeavyRows];  // weight rows 17..16 + kHeavyRows as read, when hrows > 16
