@@ -78,7 +78,7 @@ for k, (fn, _) in runs.items():
     same = all(torch.equal(a, b) for a, b in zip(snap[0], ref[0])) and torch.equal(snap[1], ref[1]) and \
         torch.equal(snap[2], ref[2])
     print(f"{k:12s} outputs identical to default: {same}  ({total / nb:.2f} symbols/block)")
-    assert same, k
+    assert same or k.startswith("no"), k  # libvar_no*.so: timing ablations, outputs knowingly wrong
 base = statistics.median(times["default"])
 for k, v in times.items():
     m = statistics.median(v)
