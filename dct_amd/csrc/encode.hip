@@ -33,7 +33,10 @@ __device__ __forceinline__ uint32_t nz16e(uint32_t w) { return ((w & 0xFFFFu) !=
 // rounds spill at this kernel's 128-VGPR bound.
 constexpr bool kEncGroup8 = true;
 constexpr int kEncWide = 0;
-constexpr int kEncGridMult = kGridMult;  // grid multiplier of this file's streaming kernels (dctq_internal.h)
+// encode_count launches 32 x its resident workgroups (about one and a half batches per wave on the
+// bench step): -1.2..-1.5 % on the whole encode step against 8 x, 48 x and 64 x the same, 16 x half
+// of it (round 6, profiles/r06/enc_count_packed_ab/enc_grid_ab*.log, tools/enc_ab.py).
+constexpr int kEncGridMult = 32;
 
 template <bool ADAPTIVE>
 __global__ __launch_bounds__(kThreads, 4) void encode_count_kernel(EncodeSet es, const DevTables *__restrict__ dev,
