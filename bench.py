@@ -955,13 +955,15 @@ def rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev, b2b=3):
                  stream (1 KiB loads, 24 x 1 KiB nt stores per 64 blocks) over the
                  workload's own pixel bytes (flat_124_const: over a constant buffer,
                  as rounds 3-5 measured it);
-      plane_124: dctq_diag_stream 11 -- flat_124's stores (the round trip's two output
-                 arrays, three drained groups) with the round trip's READ shape: each
-                 lane loads its block's 8 rows (8 B each) from a 3840-px-wide plane.
-                 Same box, same bytes: the plane's row pitch alone costs ~4 % against
-                 flat_124 (profiles/r06/INDEX.md, rt_read_shape_ab), so this, not the
-                 flat stream, is the no-arithmetic ceiling of a block transform over
-                 image planes.
+      flat_124_x32: dctq_diag_stream 16 -- the same bytes in the round trip's two output
+                 arrays with its three drained store groups, on the round trip's grid
+                 (32 x the resident workgroups): the faster flat stream on the boxes
+                 measured (profiles/r06/rt_grid_ab); fused_over_flat_124 is taken against
+                 the better of the two flat streams;
+      plane_124: dctq_diag_stream 17 -- flat_124_x32 with the round trip's READ shape: each
+                 lane loads its block's 8 rows (8 B each) from a 3840-px-wide plane, on the
+                 same grid: the no-arithmetic ceiling of a block transform over image planes
+                 (profiles/r06/INDEX.md, rt_read_shape_ab, rt_grid_ab).
     fused_over_own_movement is the kernel's time against its own data movement.
     Overwrites co/rec (run after the parity copies)."""
     import statistics
@@ -988,7 +990,8 @@ def rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev, b2b=3):
              "movement": (lambda: dplan.diag_rt_movement_planes(pls, co, rec), nblk * bpb),
              "flat_124": (lambda: flat(src), nflat * bpb),
              "flat_124_const": (lambda: flat(src7), nflat * bpb),
-             "plane_124": (lambda: flat(src, 11), nflat * bpb)}
+             "flat_124_x32": (lambda: flat(src, 16), nflat * bpb),
+             "plane_124": (lambda: flat(src, 17), nflat * bpb)}
     times = {k: [] for k in cases}
     for r in range(args.ceiling_rounds + 1):
         for k, (fn, _) in cases.items():
@@ -1004,11 +1007,13 @@ def rt_ceiling_leg(args, plan, pls, co, rec, nblk, dev, b2b=3):
     med = {k: statistics.median(v) for k, v in times.items()}
     frac = {k: cases[k][1] / med[k] / 1e9 / HBM_PEAK_GBS for k in cases}
     del src, src7, dst
+    best_flat = max(frac["flat_124"], frac["flat_124_x32"])
     return {"fused_frac": frac["fused"], "movement_frac": frac["movement"], "flat_124_frac": frac["flat_124"],
-            "flat_124_const_frac": frac["flat_124_const"], "plane_124_frac": frac["plane_124"],
+            "flat_124_x32_frac": frac["flat_124_x32"], "flat_124_const_frac": frac["flat_124_const"],
+            "plane_124_frac": frac["plane_124"],
             "fused_over_plane_124": frac["fused"] / frac["plane_124"],
             "fused_over_own_movement": frac["fused"] / frac["movement"],
-            "fused_over_flat_124": frac["fused"] / frac["flat_124"],
+            "fused_over_flat_124": frac["fused"] / best_flat,
             "fused_over_flat_124_const": frac["fused"] / frac["flat_124_const"], "rounds": args.ceiling_rounds,
             "launches_per_sample": b2b, "median_us": {k: v * 1e6 for k, v in med.items()}}
 

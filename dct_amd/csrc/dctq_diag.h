@@ -85,8 +85,10 @@ int dctq_diag_rt_movement_planes(const dctq_plan *plan, const dctq_plane *planes
  *   kind 14: kind 7 with the forward's load shape over a 3840-px-wide plane (each
  *           lane its block's 8 rows, 8 B each);
  *   kind 15: kind 11 with 16-byte loads (per instruction, rows 2k and 2k + 1 of the
- *           batch, two blocks' row slices per lane).
- * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kinds 5, 8-13: blocks *
+ *           batch, two blocks' row slices per lane);
+ *   kind 16, 17: kinds 9 / 11 on 32 x the resident grid (the round trip's), at
+ *           most one batch per wave.
+ * src >= blocks * 64 bytes, dst >= blocks * 128 bytes (kinds 5, 8-13, 15-17: blocks *
  * 384), both 16-byte aligned. */
 int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, void *stream);
 

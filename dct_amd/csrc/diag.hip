@@ -385,7 +385,20 @@ int dctq_diag_stream(int kind, const void *src, void *dst, long long blocks, voi
         break;
     }
     case 15: hipLaunchKernelGGL(stream124_rows16, dim3(grid), dim3(256), 0, s, (const uint8_t *)src, (char *)dst, nb); break;
-    default: return fail(DCTQ_EINVAL, "kind must be 0..15");
+    case 16:
+    case 17: {
+        // kinds 9 / 11 on 32 x the resident grid (the round trip's grid, round 6), capped at one
+        // batch per wave
+        const unsigned want = (nb + 3) / 4, g = (unsigned)grid * 32u;
+        if (kind == 16)
+            hipLaunchKernelGGL(stream124_split<true>, dim3(g < want ? g : want), dim3(256), 0, s, (const u4v *)src,
+                               (char *)dst, nb);
+        else
+            hipLaunchKernelGGL(stream124_rows<3840>, dim3(g < want ? g : want), dim3(256), 0, s,
+                               (const uint8_t *)src, (char *)dst, nb);
+        break;
+    }
+    default: return fail(DCTQ_EINVAL, "kind must be 0..17");
     }
     HIPCHK(hipGetLastError(), "diag stream launch");
     return DCTQ_OK;

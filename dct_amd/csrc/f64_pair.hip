@@ -210,12 +210,18 @@ __global__ __launch_bounds__(kThreadsP, 4) void idct8_pair(const DevTables *__re
     }
 }
 
+// Both paired kernels launch up to 64 x their resident workgroups (about one 32-block batch per
+// wave on 4K-frame stacks): round 6, tools/pair_ab.py, three passes, 64 4K frames: dctq_inverse
+// -1.2..-3.7 % and dctq_forward_float -4.2..-4.7 % against 8 x (32 x / 48 x in between; 16 x made
+// the forward 4-5 % slower), profiles/r06/pair_grid_ab/.
+constexpr int kPairGridMult = 64;
+
 template <typename K, typename... A>
 static hipError_t launch_persistent(K kernel, long long nblk, int num_cus, hipStream_t stream, A... args) {
     const int per_cu = resident_per_cu(kernel, kThreadsP);
     const long long nbatch = (nblk + 31) / 32;
     const long long want = (nbatch + kWavesP - 1) / kWavesP;
-    const long long cap = (long long)num_cus * per_cu * kGridMult;
+    const long long cap = (long long)num_cus * per_cu * kPairGridMult;
     hipLaunchKernelGGL(kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(kThreadsP), 0, stream, args...);
     return hipGetLastError();
 }

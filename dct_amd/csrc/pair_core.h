@@ -11,7 +11,10 @@ constexpr int kWavesP = 4;
 constexpr int kThreadsP = 64 * kWavesP;
 constexpr int kPitchP = 272;          // bytes per block in the stage: 256 + 16 (b128 writes spread over the banks)
 constexpr int kRtOcc = 4;             // the fused round trip's waves per SIMD (launch bound)
-constexpr int kRtGridMult = kGridMult;  // ... and its grid multiplier (dctq_internal.h)
+// ... and its grid multiplier: 32 x the resident workgroups (round 6, tools/rt_ab.py, interleaved,
+// both orders: 8 x +3.0..+3.5 %, 16 x +2.2..+2.4 %, 24 x +1.3..+1.4 %, 48 x -0.6..-1.1 %, 64 x +1.2 %
+// against 32 x; profiles/r06/rt_grid_ab/)
+constexpr int kRtGridMult = 32;
 
 typedef uint32_t u2p __attribute__((ext_vector_type(2)));
 typedef uint32_t u4p __attribute__((ext_vector_type(4)));

@@ -784,7 +784,7 @@ def test_diag_stream_moves_bytes(T, dm):
     roofline.movement_ceiling) move what they claim: the flat 1:2 stream writes
     each 1 KiB input chunk twice (the second copy with bit 0 of its first dword
     flipped), the write-only stream covers the whole output; the round trip's 1:2:4
-    streams (kinds 5, 8-13, 15) and the plane-read 1:2 stream (14) run and write."""
+    streams (kinds 5, 8-13, 15-17) and the plane-read 1:2 stream (14) run and write."""
     D = dm.diag()
     n = 64 * 40
     src = T.randint(0, 256, (n * 64,), dtype=T.uint8, device="cuda")
@@ -809,14 +809,14 @@ def test_diag_stream_moves_bytes(T, dm):
     # the round trip's streams (1:2:4 bytes): the same bytes in the two-array layout with
     # and without the drained store groups; the plane-read streams in any batch order
     out = {}
-    for kind in (5, 8, 9, 10, 11, 12, 13, 15):
+    for kind in (5, 8, 9, 10, 11, 12, 13, 15, 16, 17):
         dst = T.zeros(n * 384, dtype=T.uint8, device="cuda")
         assert D.dctq_diag_stream(kind, src.data_ptr(), dst.data_ptr(), n, s) == 0, kind
         T.cuda.synchronize()
         out[kind] = dst.cpu().numpy()
         assert out[kind].any(), kind
-    assert np.array_equal(out[8], out[9])
-    assert np.array_equal(out[11], out[12]) and np.array_equal(out[11], out[13])
+    assert np.array_equal(out[8], out[9]) and np.array_equal(out[9], out[16])
+    assert np.array_equal(out[11], out[12]) and np.array_equal(out[11], out[13]) and np.array_equal(out[11], out[17])
     a = src.view(-1, 4, 1024).cpu().numpy()  # kind 8: region A holds each batch's 4 KiB twice (bit 0 of dword 0 flipped)
     ra = out[8][:n * 128].reshape(-1, 8, 1024)
     assert np.array_equal(ra[:, 0::2], a)
@@ -824,7 +824,7 @@ def test_diag_stream_moves_bytes(T, dm):
     assert D.dctq_diag_stream(14, src.data_ptr(), dst.data_ptr(), n, s) == 0
     T.cuda.synchronize()
     assert dst.cpu().numpy().any()
-    assert D.dctq_diag_stream(16, src.data_ptr(), dst.data_ptr(), n, s) != 0
+    assert D.dctq_diag_stream(18, src.data_ptr(), dst.data_ptr(), n, s) != 0
 
 
 def _sym32(sym):

@@ -12,7 +12,7 @@ two-array output layout: coefficients and recon in separate regions), "flat2g" (
 trip's three store groups and their drains), "rows8" (flat2g with the round trip's load shape: 8-byte row
 loads per lane, the batch contiguous), "rows2d" (rows8 over a 3840-px-wide plane: the luma row pitch), "rows2d_wg" / "rows2d_wave" (rows2d
 with workgroup- / wave-contiguous runs of batches), "rows2d16" (rows2d with 16-byte loads, two rows per
-instruction), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
+instruction), "flat2g32" / "rows2d32" (flat2g / rows2d on 32 x the resident grid), "mv" (the diagnostic library's movement twin), or "mv:PATH" /
 "fused:PATH" (those of a build at PATH, tools/ubench/variant.sh, DIAG=1 for mv).
 Default: fused fused64 flat mv.
 """
@@ -69,10 +69,10 @@ def lib_plan(path, inverse=None):
 runs = {}
 for e in args.entries:
     kind, _, path = e.partition(":")
-    if kind in ("flat", "flatpx", "flat2", "flat2g", "rows8", "rows2d", "rows2d_wg", "rows2d_wave", "rows2d16"):
+    if kind in ("flat", "flatpx", "flat2", "flat2g", "rows8", "rows2d", "rows2d_wg", "rows2d_wave", "rows2d16", "flat2g32", "rows2d32"):
         D = dct_amd.diag()
         buf = src if kind == "flat" else srcpx
-        sk = {"flat": 5, "flatpx": 5, "flat2": 8, "flat2g": 9, "rows8": 10, "rows2d": 11, "rows2d_wg": 12, "rows2d_wave": 13, "rows2d16": 15}[kind]
+        sk = {"flat": 5, "flatpx": 5, "flat2": 8, "flat2g": 9, "rows8": 10, "rows2d": 11, "rows2d_wg": 12, "rows2d_wave": 13, "rows2d16": 15, "flat2g32": 16, "rows2d32": 17}[kind]
         runs[e] = lambda D=D, buf=buf, sk=sk: D.dctq_diag_stream(sk, buf.data_ptr(), dst.data_ptr(), nflat, stream)
         continue
     if kind in ("fused", "fused64"):
