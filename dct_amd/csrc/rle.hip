@@ -751,8 +751,11 @@ hipError_t launch_rle_count(const int16_t *coef, long long nblk, uint32_t *offse
 hipError_t launch_rle_emit(const int16_t *coef, long long nblk, const uint32_t *offsets, void *symbols,
                            int symbol_bytes, unsigned long long capacity, hipStream_t stream, int num_cus) {
     const long long ntiles = (nblk + 63) / 64;
+    // 2-byte emit: up to 1 024 workgroups per CU (about one tile per wave on the bench step):
+    // -2.3..-2.9 % on the encode step against 64 (round 6, profiles/r06/rle_grid_ab/, tools/enc_ab.py);
+    // the 4-byte emit was 5 % slower that way (tools/rle_ab.py), and the decoders 5-17 %, so they keep 64
     if (symbol_bytes == 2)
-        hipLaunchKernelGGL(rle_emit_kernel<2>, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, coef,
+        hipLaunchKernelGGL(rle_emit_kernel<2>, dim3(grid_for(ntiles, num_cus, 1024)), dim3(kRleThreads), 0, stream, coef,
                            nblk, offsets, symbols, ntiles, capacity);
     else
         hipLaunchKernelGGL(rle_emit_kernel<4>, dim3(grid_for(ntiles, num_cus, 64)), dim3(kRleThreads), 0, stream, coef,
